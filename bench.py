@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpix/s of per-view depth on synthetic 5-view 1080p
+stacks, 128 disparity hypotheses, NCC 5x5, SLIC K~2000 (BASELINE.json config 2).
+
+One step = the whole depth pipeline over one batch: for each of the V reference
+views of this rank's stack (inputs RGBx already resident in HBM): Lab
+conversion, SLIC (S=32, 5 update/assign iterations), superpixel extents, the
+reference superpixel SAD sweep, the per-pixel NCC 5x5 cost volume over 128
+hypotheses x 4 neighbours and its winner-take-all + confidence pass.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--cost ncc|sad]
+
+N>1: launched by torch.distributed.run, one rank per GPU; every rank owns its
+own 5-view stack (independent objects, no data-path collective) -> weak scaling.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (array w, h, W, H, S, dmin, dmax, K, nh, nv, bl)
+    "c1": dict(aw=2, ah=1, W=640, H=480, S=1, dmin=0, dmax=31, K=5, nh=1, nv=0, bl=1.0, cost="sad",
+               workload="2-view 640x480, 32 hypotheses, SAD 5x5, SLIC off (reference per-pixel sweep)"),
+    "c2": dict(aw=5, ah=1, W=1920, H=1080, S=32, dmin=0, dmax=127, K=5, nh=4, nv=0, bl=1.0, cost="ncc",
+               workload="5-view 1920x1080, 128 hypotheses, NCC 5x5, SLIC K=2040 (S=32), 1 GPU per 5-view stack"),
+    "c5": dict(aw=5, ah=1, W=4096, H=3072, S=40, dmin=0, dmax=255, K=7, nh=4, nv=0, bl=1.0, cost="ncc",
+               workload="5-view 4096x3072, 256 hypotheses, NCC 7x7, SLIC K=7931 (S=40)"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cost", default=None, choices=["ncc", "sad"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from cl_multiview_stereo_amd import params, synth
+    from cl_multiview_stereo_amd.engine import Engine
+    from cl_multiview_stereo_amd.pipeline import Pipeline
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfg = dict(CONFIGS[args.config])
+    cost = args.cost or cfg["cost"]
+    V = cfg["aw"] * cfg["ah"]
+    W, H = cfg["W"], cfg["H"]
+    st = params.Settings(spixl_size=cfg["S"], array_width=cfg["aw"], array_height=cfg["ah"], min_disp=cfg["dmin"],
+                         max_disp=cfg["dmax"], inc=1, neib_hor=cfg["nh"], neib_ver=cfg["nv"], bl_ratio=cfg["bl"],
+                         window=cfg["K"], cost=cost)
+    D = cfg["dmax"] - cfg["dmin"] + 1
+
+    e = Engine(local)
+    stack, _ = synth.make_stack(W, H, cfg["aw"], cfg["ah"], cfg["dmin"], cfg["dmax"], cfg["bl"],
+                                0x5EED + 2 + rank)
+    rgbx = torch.from_numpy(stack).to(e.device)
+    pipe = Pipeline(e, st, W, H, pixel_cost=cost)
+
+    # HIP events around the cost-volume kernels, on the stream they run on
+    timers = {"wta": [], "ncc": []}
+    if pipe.pixel is not None and cost == "ncc":
+        orig_wta, orig_vol = e.wta, e.ncc_volume
+
+        def timed(name, fn):
+            def w(*a, **k):
+                s = torch.cuda.Event(enable_timing=True)
+                t = torch.cuda.Event(enable_timing=True)
+                s.record()
+                r = fn(*a, **k)
+                t.record()
+                if timing[0]:
+                    timers[name].append((s, t))
+                return r
+            return w
+        timing = [False]
+        e.wta = timed("wta", orig_wta)
+        e.ncc_volume = timed("ncc", orig_vol)
+    else:
+        timing = [False]
+
+    def step():
+        return pipe.exe_pipeline(rgbx)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timing[0] = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    timing[0] = False
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=e.device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed * 1e3 / max(args.steps, 1)
+    mpix = world * V * W * H * args.steps / elapsed / 1e6
+
+    res = {
+        "metric": "Mpix/s depth (1080p, 128 depth hyp, 5 views) + depth L1 vs ref",
+        "value": round(mpix, 3),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32/i32",
+        "data": "synthetic (seeded rendered camera-array stack, RGBx resident in HBM)",
+        "config": {"workload": cfg["workload"], "views": V, "width": W, "height": H, "hypotheses": D,
+                   "window": cfg["K"], "cost": cost, "spixl_size": cfg["S"], "neighbours": cfg["nh"],
+                   "parallelism": f"view-stack per GPU x{world}"},
+    }
+
+    if timers["wta"]:
+        def avg(lst):
+            return sum(s.elapsed_time(t) for s, t in lst) / len(lst) * 1e-3
+        t_wta = avg(timers["wta"])
+        t_ncc = avg(timers["ncc"])
+        wta_bytes = 4.0 * D * W * H + 8.0 * W * H  # volume read + disparity/confidence write
+        achieved = wta_bytes / t_wta / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_wta.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res["roofline"] = {"bound": "hbm", "kernel": "k_wta (cost-volume read pass)", "achieved": round(achieved, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                           "traffic": traffic, "algorithmic_bytes_per_launch": wta_bytes,
+                           "avg_launch_ms": round(t_wta * 1e3, 4)}
+        cells = float(D) * W * H
+        nbr = cfg["nh"] if cfg["aw"] > 1 else 1
+        vol_bytes = 4.0 * cells
+        res["roofline_sweep"] = {"kernel": "k_ncc_volume (cost-volume write pass)", "avg_launch_ms": round(t_ncc * 1e3, 4),
+                                 "view_cells_per_s": round(cells * nbr / t_ncc / 1e9, 3),
+                                 "unit_view_cells": "G view-cells/s",
+                                 "hbm_write_GBps": round(vol_bytes / t_ncc / 1e9, 1),
+                                 "hbm_write_frac": round(vol_bytes / t_ncc / 1e9 / HBM_PEAK_GBS, 4)}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            res["cpu_baseline"], res["depth_l1_vs_oracle"] = cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out)
+        except Exception as ex:  # report, never hide
+            res["cpu_baseline"] = {"error": repr(ex)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out):
+    """Oracle (CPU restatement, OpenMP) on a bounded sample of the same
+    workload; returns (cpu_baseline dict, depth L1 of the GPU vs the oracle)."""
+    import torch
+
+    from cl_multiview_stereo_amd import params
+    from oracle import oracle as orc
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    W, H, S = cfg["W"], cfg["H"], cfg["S"]
+    levels = pipe.cam.levels
+    Dfull = len(levels)
+    Dsub = min(Dfull, 16)
+    sub = levels[:Dsub]
+    t0 = time.perf_counter()
+    # one reference view: cvt + SLIC of all views it needs, boundary, sweep, NCC volume on Dsub levels, WTA
+    labs, sps, lbs = [], [], []
+    for v in range(stack.shape[0]):
+        if S > 1:
+            lab, sp, lb = orc.slic(stack[v], S)
+        else:
+            lab, sp, lb = orc.grid(stack[v], 1)
+        labs.append(lab); sps.append(sp); lbs.append(lb)
+    t_slic = time.perf_counter() - t0
+    lab_all = np.stack(labs)
+    t1 = time.perf_counter()
+    if cost == "ncc":
+        q = orc.l8(lab_all)
+        vol = orc.ncc_volume(q, sub, pipe.cam.view_subset, pipe.cam.subset_num, cfg["aw"], cfg["bl"], cfg["K"], 0)
+        od, _ = orc.wta(vol, sub)
+    else:
+        od = orc.sweep_pixel_sad(lab_all, sub, pipe.cam.view_subset, pipe.cam.subset_num, cfg["aw"], cfg["bl"], 0, 1)[0]
+    t_sweep = time.perf_counter() - t1
+    # per reference view at the full hypothesis count: SLIC share + sweep scaled Dfull/Dsub
+    V = stack.shape[0]
+    t_view = t_slic / V + t_sweep * (Dfull / Dsub)
+    cpu = {"value": round(W * H / t_view / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/mvs_oracle.c on 1 reference view: SLIC of all {V} views ({t_slic:.2f}s, /{V} per view) "
+                     f"+ {cost.upper()} sweep over {Dsub} of {Dfull} hypotheses ({t_sweep:.2f}s, x{Dfull / Dsub:g})"}
+    # depth L1 on the same sample: GPU sweep of reference view 0 over the same subset
+    from cl_multiview_stereo_amd.engine import CameraArray
+    cam = CameraArray(cfg["aw"], cfg["bl"], sub, pipe.cam.view_subset, pipe.cam.subset_num)
+    lab, l8 = e.cvt(rgbx)
+    if cost == "ncc":
+        box = e.box_stats(l8, cfg["K"])
+        vol_g = e.ncc_volume(l8, box, cam, 0, cfg["K"])
+        gd, _ = e.wta(vol_g, e.levels_dev(cam))
+    else:
+        gd = e.sweep_pixel_sad(lab, cam, 0, 1)[0]
+    torch.cuda.synchronize()
+    l1 = float(np.abs(gd.cpu().numpy() - od).mean())
+    return cpu, {"value": l1, "unit": "px (mean |d_gpu - d_oracle|)",
+                 "sample": f"reference view 0, {Dsub} hypotheses, full {W}x{H}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,418 @@
+// C-ABI of libmvs.so (include/mvs.h): context management, argument checking,
+// metadata upload and the stage orchestration that the reference's host stage
+// classes perform (clSLIC, clPhotoConsistency, clDepthRefinement).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mvs_internal.h"
+
+namespace {
+thread_local std::string g_err;
+
+template <class T>
+int ensure_dev(T** p, size_t* cap, size_t n) {
+  if (*cap >= n && *p) return 0;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc((void**)p, sizeof(T) * (n ? n : 1)) != hipSuccess) {
+    mvs::set_error("hipMalloc failed for metadata");
+    return MVS_E_NOMEM;
+  }
+  *cap = n;
+  return 0;
+}
+
+int check_array(const mvs_array* a) {
+  if (!a || a->view_count <= 0 || a->array_width <= 0 || !a->levels || a->num_levels <= 0 || !a->view_subset ||
+      !a->subset_num)
+    return mvs::arg_fail("mvs_array: null pointer or non-positive size");
+  for (int z = 0; z < a->view_count; z++) {
+    int n = a->subset_num[z];
+    if (n < 0 || n > a->view_count) return mvs::arg_fail("mvs_array: subset_num out of range");
+    for (int k = 0; k < n; k++) {
+      int v = a->view_subset[a->view_count * z + k];
+      if (v < 0 || v >= a->view_count) return mvs::arg_fail("mvs_array: view_subset entry out of range");
+    }
+  }
+  return 0;
+}
+
+// Upload levels / view_subset / subset_num when they differ from the cached copy.
+int upload_meta(mvs_ctx* c, const mvs_array* a) {
+  int rc = check_array(a);
+  if (rc) return rc;
+  int V = a->view_count, D = a->num_levels;
+  bool same = (int)c->h_levels.size() == D && (int)c->h_sn.size() == V &&
+              std::memcmp(c->h_levels.data(), a->levels, sizeof(float) * D) == 0 &&
+              std::memcmp(c->h_vs.data(), a->view_subset, sizeof(int) * V * V) == 0 &&
+              std::memcmp(c->h_sn.data(), a->subset_num, sizeof(int) * V) == 0;
+  if (same) return 0;
+  if ((rc = ensure_dev(&c->d_levels, &c->cap_levels, (size_t)D))) return rc;
+  if ((rc = ensure_dev(&c->d_vs, &c->cap_vs, (size_t)V * V))) return rc;
+  if ((rc = ensure_dev(&c->d_sn, &c->cap_sn, (size_t)V))) return rc;
+  c->h_levels.assign(a->levels, a->levels + D);
+  c->h_vs.assign(a->view_subset, a->view_subset + (size_t)V * V);
+  c->h_sn.assign(a->subset_num, a->subset_num + V);
+  MVS_HIP(hipMemcpyAsync(c->d_levels, c->h_levels.data(), sizeof(float) * D, hipMemcpyHostToDevice, c->stream),
+          "upload levels");
+  MVS_HIP(hipMemcpyAsync(c->d_vs, c->h_vs.data(), sizeof(int) * V * V, hipMemcpyHostToDevice, c->stream),
+          "upload view_subset");
+  MVS_HIP(hipMemcpyAsync(c->d_sn, c->h_sn.data(), sizeof(int) * V, hipMemcpyHostToDevice, c->stream),
+          "upload subset_num");
+  // the host vectors are the copy sources: finish before they can change
+  MVS_HIP(hipStreamSynchronize(c->stream), "upload sync");
+  return 0;
+}
+
+bool bad_dims(int W, int H) { return W <= 0 || H <= 0 || (long)W * H > (1L << 31) / 16; }
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) hipFree(p);
+  }
+  int alloc(size_t n) {
+    if (hipMalloc(&p, n ? n : 1) != hipSuccess) {
+      mvs::set_error("hipMalloc failed");
+      return MVS_E_NOMEM;
+    }
+    return 0;
+  }
+  template <class T>
+  T* as() {
+    return (T*)p;
+  }
+};
+
+}  // namespace
+
+namespace mvs {
+void set_error(const std::string& msg) { g_err = msg; }
+int hip_fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return MVS_E_HIP;
+}
+int arg_fail(const char* what) {
+  g_err = what;
+  return MVS_E_ARG;
+}
+void* scratch(mvs_ctx* ctx, size_t bytes, int* rc) {
+  *rc = 0;
+  if (ctx->scratch_bytes >= bytes && ctx->scratch) return ctx->scratch;
+  if (ctx->scratch) {
+    hipStreamSynchronize(ctx->stream);
+    hipFree(ctx->scratch);
+  }
+  ctx->scratch = nullptr;
+  ctx->scratch_bytes = 0;
+  if (hipMalloc(&ctx->scratch, bytes) != hipSuccess) {
+    *rc = MVS_E_NOMEM;
+    g_err = "scratch allocation failed";
+    return nullptr;
+  }
+  ctx->scratch_bytes = bytes;
+  return ctx->scratch;
+}
+}  // namespace mvs
+
+#define RC(x)           \
+  do {                  \
+    int _r = (x);       \
+    if (_r) return _r;  \
+  } while (0)
+
+extern "C" {
+
+const char* mvs_last_error(void) { return g_err.c_str(); }
+const char* mvs_version(void) { return "mvs-mi355x 0.1 (gfx950)"; }
+
+int mvs_create(int device, mvs_ctx** out) {
+  if (!out) return mvs::arg_fail("mvs_create: out is null");
+  int n = 0;
+  MVS_HIP(hipGetDeviceCount(&n), "hipGetDeviceCount");
+  if (device < 0 || device >= n) return mvs::arg_fail("mvs_create: no such device");
+  MVS_HIP(hipSetDevice(device), "hipSetDevice");
+  mvs_ctx* c = new mvs_ctx();
+  c->device = device;
+  *out = c;
+  return 0;
+}
+
+void mvs_destroy(mvs_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  if (c->scratch) hipFree(c->scratch);
+  if (c->d_levels) hipFree(c->d_levels);
+  if (c->d_vs) hipFree(c->d_vs);
+  if (c->d_sn) hipFree(c->d_sn);
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int mvs_set_stream(mvs_ctx* c, void* s) {
+  if (!c) return mvs::arg_fail("null context");
+  c->stream = (hipStream_t)s;
+  return 0;
+}
+
+int mvs_synchronize(mvs_ctx* c) {
+  if (!c) return mvs::arg_fail("null context");
+  MVS_HIP(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  return 0;
+}
+
+// ---- device-pointer API ------------------------------------------------------
+int mvs_cvt_d(mvs_ctx* c, const uint8_t* rgbx, int V, int W, int H, float* lab, uint8_t* l8) {
+  if (!c || !rgbx || !lab || V <= 0 || bad_dims(W, H)) return mvs::arg_fail("mvs_cvt_d: bad arguments");
+  return mvs::launch_cvt(c->stream, rgbx, (long)V * W * H, lab, l8);
+}
+
+int mvs_grid_d(mvs_ctx* c, const float* lab, int V, int W, int H, int S, float* spixl, uint32_t* labels) {
+  if (!c || !lab || !spixl || !labels || V <= 0 || S <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_grid_d: bad arguments");
+  RC(mvs::launch_init_centers(c->stream, lab, V, W, H, S, spixl));
+  return mvs::launch_grid_labels(c->stream, V, W, H, S, labels);
+}
+
+int mvs_slic_d(mvs_ctx* c, const float* lab, int V, int W, int H, const mvs_slic_params* p, float* spixl,
+               uint32_t* labels) {
+  if (!c || !lab || !spixl || !labels || !p || V <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_slic_d: bad arguments");
+  int S = p->spixl_size;
+  if (S < 6 || S > 96) return mvs::arg_fail("mvs_slic_d: spixl_size must be in [6, 96] (3S/16 > 0)");
+  if (p->no_iter < 0) return mvs::arg_fail("mvs_slic_d: no_iter < 0");
+  // clSLIC ctor, clSLIC.cpp:15-18 (host float arithmetic)
+  float xy = 1.0f / (1.4242f * (float)S);
+  float col = 15.0f / (1.7321f * 128.0f);
+  xy = xy * xy;
+  col = col * col;
+  hipStream_t s = c->stream;
+  RC(mvs::launch_init_centers(s, lab, V, W, H, S, spixl));
+  RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
+  for (int i = 0; i < p->no_iter; i++) {
+    RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl));
+    RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
+  }
+  if (p->enforce_connectivity) {
+    int rc = 0;
+    uint32_t* tmp = (uint32_t*)mvs::scratch(c, sizeof(uint32_t) * (size_t)V * W * H, &rc);
+    if (rc) return rc;
+    RC(mvs::launch_suppress(s, labels, tmp, V, W, H));
+    RC(mvs::launch_suppress(s, tmp, labels, V, W, H));
+  }
+  return 0;
+}
+
+int mvs_boundary_d(mvs_ctx* c, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                   uint8_t* rep) {
+  if (!c || !spixl || !labels || !rep || V <= 0 || S <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_boundary_d: bad arguments");
+  if (S > 256) return mvs::arg_fail("mvs_boundary_d: extents are uint8 (S <= 256)");
+  return mvs::launch_boundary(c->stream, V, W, H, S, spixl, labels, rep);
+}
+
+int mvs_sweep_spixl_d(mvs_ctx* c, int W, int H, int S, const float* lab, float* spixl, const uint8_t* rep,
+                      const mvs_array* a, int z0, int z1) {
+  if (!c || !lab || !spixl || !rep || S <= 0 || bad_dims(W, H)) return mvs::arg_fail("mvs_sweep_spixl_d: bad arguments");
+  RC(upload_meta(c, a));
+  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_sweep_spixl_d: bad view range");
+  return mvs::launch_sweep_spixl(c->stream, a->view_count, W, H, S, lab, spixl, rep, c->d_levels, a->num_levels,
+                                 c->d_vs, c->d_sn, a->array_width, a->bl_ratio, z0, z1);
+}
+
+int mvs_sweep_pixel_sad_d(mvs_ctx* c, int W, int H, const float* lab, const mvs_array* a, int z0, int z1,
+                          float* disp) {
+  if (!c || !lab || !disp || bad_dims(W, H)) return mvs::arg_fail("mvs_sweep_pixel_sad_d: bad arguments");
+  RC(upload_meta(c, a));
+  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_sweep_pixel_sad_d: bad view range");
+  return mvs::launch_sweep_pixel_sad(c->stream, a->view_count, W, H, lab, c->d_levels, a->num_levels, c->d_vs,
+                                     c->d_sn, a->subset_num, a->array_width, a->bl_ratio, z0, z1, disp);
+}
+
+int mvs_box_stats_d(mvs_ctx* c, const uint8_t* l8, int V, int W, int H, int K, int32_t* box) {
+  if (!c || !l8 || !box || V <= 0 || bad_dims(W, H) || (K != 5 && K != 7))
+    return mvs::arg_fail("mvs_box_stats_d: bad arguments (K must be 5 or 7)");
+  return mvs::launch_box_stats(c->stream, l8, V, W, H, K, box);
+}
+
+int mvs_ncc_volume_d(mvs_ctx* c, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a, int K,
+                     int z, float* vol) {
+  if (!c || !l8 || !box || !vol || bad_dims(W, H)) return mvs::arg_fail("mvs_ncc_volume_d: bad arguments");
+  RC(upload_meta(c, a));
+  if (z < 0 || z >= a->view_count) return mvs::arg_fail("mvs_ncc_volume_d: bad reference view");
+  return mvs::launch_ncc_volume(c->stream, a->view_count, W, H, l8, box, c->d_levels, a->num_levels,
+                                a->view_subset, a->subset_num, a->array_width, a->bl_ratio, K, z, vol);
+}
+
+int mvs_wta_d(mvs_ctx* c, int W, int H, int D, const float* vol, const float* levels, float* disp, float* conf) {
+  if (!c || !vol || !levels || !disp || D <= 0 || bad_dims(W, H)) return mvs::arg_fail("mvs_wta_d: bad arguments");
+  return mvs::launch_wta(c->stream, W, H, D, vol, levels, disp, conf);
+}
+
+int mvs_flatness_d(mvs_ctx* c, int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
+  if (!c || !spixl || !flat || V <= 0 || mw <= 0 || mh <= 0) return mvs::arg_fail("mvs_flatness_d: bad arguments");
+  return mvs::launch_flatness(c->stream, V, mw, mh, spixl, gamma, flat);
+}
+
+int mvs_init_state_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels, const uint8_t* rep,
+                     const float* flat, const mvs_array* a, float gamma, float alpha, int kernel_steps, float kss,
+                     float fuse, float* state) {
+  if (!c || !spixl || !labels || !rep || !flat || !state || S <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_init_state_d: bad arguments");
+  RC(upload_meta(c, a));
+  return mvs::launch_init_state(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, rep,
+                                flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state);
+}
+
+int mvs_propagate_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels, const uint8_t* rep,
+                    const float* flat, const mvs_array* a, int iter, float alpha, float gamma, float fuse,
+                    int kernel_steps, float kss, const float* st_in, float* st_out, int z0, int z1) {
+  if (!c || !spixl || !labels || !rep || !flat || !st_in || !st_out || S <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_propagate_d: bad arguments");
+  RC(upload_meta(c, a));
+  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_propagate_d: bad view range");
+  return mvs::launch_propagate(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, rep,
+                               flat, c->d_vs, c->d_sn, iter, alpha, gamma, fuse, kernel_steps, kss, st_in, st_out,
+                               z0, z1);
+}
+
+int mvs_spixl_to_image_d(mvs_ctx* c, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                         const float* state, float* disp) {
+  if (!c || !spixl || !labels || !state || !disp || V <= 0 || S <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_spixl_to_image_d: bad arguments");
+  return mvs::launch_spixl_to_image(c->stream, V, W, H, S, spixl, labels, state, disp);
+}
+
+// clDepthRefinement::do_refinement + fusion (depth_refinement.cpp:91-118, 1318-1370)
+int mvs_refine_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels, const uint8_t* rep,
+                 const mvs_array* a, const mvs_refine_params* p, float* flat, float* state, float* state2,
+                 float* disp) {
+  if (!c || !p || !flat || !state || !state2) return mvs::arg_fail("mvs_refine_d: bad arguments");
+  RC(upload_meta(c, a));
+  int V = a->view_count;
+  int mw = mvs::map_dim(W, S), mh = mvs::map_dim(H, S);
+  // pipeline::refine_depth_map, pipeline.cpp:164-166
+  float gamma_ = (float)(2.0 * std::pow((double)p->gamma, 2.0));
+  float alpha_ = (float)(2.0 * std::pow((double)p->alpha, 2.0));
+  int kernel_size = p->kernel_size / 2;
+  int nks = p->kernel_step;
+  if (nks <= 0) return mvs::arg_fail("mvs_refine_d: kernel_step must be > 0");
+  int kss_i = kernel_size / nks * S;
+  float kss = (float)(kss_i > 1 ? kss_i : 1);
+  float fuse = (float)(0.5 * (double)p->fuse);
+  RC(mvs_flatness_d(c, V, mw, mh, spixl, (float)(1.0 / (double)gamma_), flat));
+  RC(mvs_init_state_d(c, W, H, S, spixl, labels, rep, flat, a, 1.0f / gamma_, 1.0f / alpha_, nks, kss, fuse, state));
+  float pg = (float)(1.0 / (double)gamma_), pa = (float)(1.0 / (double)alpha_);
+  size_t sb = sizeof(float) * 6 * (size_t)V * mw * mh;
+  if (p->no_prop > 0) MVS_HIP(hipMemcpyAsync(state2, state, sb, hipMemcpyDeviceToDevice, c->stream), "copy state");
+  for (int it = 0; it < p->no_prop; it++) {
+    float* out = (it % 2 == 0) ? state2 : state;
+    const float* in = (it % 2 == 0) ? state : state2;
+    RC(mvs_propagate_d(c, W, H, S, spixl, labels, rep, flat, a, it, pa, pg, fuse, nks / (it + 1),
+                       kss / (float)(it + 1), in, out, 0, V));
+  }
+  // fusion renders current_state_dev (= `state`): the last odd iteration
+  // (reference behaviour, Appendix A #13); non-compat renders the final one.
+  const float* src = state;
+  if (!p->fusion_compat && p->no_prop > 0) src = ((p->no_prop - 1) % 2 == 0) ? state2 : state;
+  if (disp) RC(mvs_spixl_to_image_d(c, V, W, H, S, spixl, labels, src, disp));
+  return 0;
+}
+
+int mvs_filter_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, float fuse, const float* disp_full,
+                 float* proj, float* out, int z0, int z1) {
+  if (!c || !disp_full || !proj || !out || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V ||
+      z0 > z1)
+    return mvs::arg_fail("mvs_filter_d: bad arguments");
+  return mvs::launch_filter(c->stream, V, W, H, array_width, bl_ratio, (float)(0.5 * (double)fuse), disp_full, proj,
+                            out, z0, z1);
+}
+
+// ---- host-pointer API (reference stage methods) ----------------------------------
+int mvs_do_super_pixel_seg(mvs_ctx* c, const uint8_t* rgbx, int W, int H, const mvs_slic_params* p, float* lab,
+                           float* spixl, uint32_t* labels) {
+  if (!c || !rgbx || !p || bad_dims(W, H) || p->spixl_size <= 0) return mvs::arg_fail("mvs_do_super_pixel_seg: bad arguments");
+  size_t P = (size_t)W * H;
+  int mw = mvs::map_dim(W, p->spixl_size), mh = mvs::map_dim(H, p->spixl_size);
+  size_t M = (size_t)mw * mh;
+  DevBuf din, dlab, dsp, dlb;
+  RC(din.alloc(P * 4));
+  RC(dlab.alloc(P * 16));
+  RC(dsp.alloc(M * 32));
+  RC(dlb.alloc(P * 4));
+  hipStream_t s = c->stream;
+  MVS_HIP(hipMemsetAsync(dsp.p, 0, M * 32, s), "memset");
+  MVS_HIP(hipMemcpyAsync(din.p, rgbx, P * 4, hipMemcpyHostToDevice, s), "H2D rgbx");
+  RC(mvs_cvt_d(c, din.as<uint8_t>(), 1, W, H, dlab.as<float>(), nullptr));
+  RC(mvs_slic_d(c, dlab.as<float>(), 1, W, H, p, dsp.as<float>(), dlb.as<uint32_t>()));
+  if (lab) MVS_HIP(hipMemcpyAsync(lab, dlab.p, P * 16, hipMemcpyDeviceToHost, s), "D2H lab");
+  if (spixl) MVS_HIP(hipMemcpyAsync(spixl, dsp.p, M * 32, hipMemcpyDeviceToHost, s), "D2H spixl");
+  if (labels) MVS_HIP(hipMemcpyAsync(labels, dlb.p, P * 4, hipMemcpyDeviceToHost, s), "D2H labels");
+  MVS_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
+int mvs_do_initial_depth_estimation(mvs_ctx* c, int W, int H, int S, float* spixl, uint8_t* rep, const float* lab,
+                                    const uint32_t* labels, const mvs_array* a) {
+  if (!c || !spixl || !lab || !labels || S <= 0 || bad_dims(W, H)) return mvs::arg_fail("mvs_do_initial_depth_estimation: bad arguments");
+  RC(check_array(a));
+  int V = a->view_count;
+  size_t P = (size_t)W * H;
+  int mw = mvs::map_dim(W, S), mh = mvs::map_dim(H, S);
+  size_t M = (size_t)mw * mh;
+  DevBuf dlab, dsp, dlb, drep;
+  RC(dlab.alloc(V * P * 16));
+  RC(dsp.alloc(V * M * 32));
+  RC(dlb.alloc(V * P * 4));
+  RC(drep.alloc(V * M * 8));
+  hipStream_t s = c->stream;
+  MVS_HIP(hipMemcpyAsync(dlab.p, lab, V * P * 16, hipMemcpyHostToDevice, s), "H2D lab");
+  MVS_HIP(hipMemcpyAsync(dsp.p, spixl, V * M * 32, hipMemcpyHostToDevice, s), "H2D spixl");
+  MVS_HIP(hipMemcpyAsync(dlb.p, labels, V * P * 4, hipMemcpyHostToDevice, s), "H2D labels");
+  RC(mvs_boundary_d(c, V, W, H, S, dsp.as<float>(), dlb.as<uint32_t>(), drep.as<uint8_t>()));
+  RC(mvs_sweep_spixl_d(c, W, H, S, dlab.as<float>(), dsp.as<float>(), drep.as<uint8_t>(), a, 0, V));
+  MVS_HIP(hipMemcpyAsync(spixl, dsp.p, V * M * 32, hipMemcpyDeviceToHost, s), "D2H spixl");
+  if (rep) MVS_HIP(hipMemcpyAsync(rep, drep.p, V * M * 8, hipMemcpyDeviceToHost, s), "D2H rep");
+  MVS_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
+int mvs_do_refinement(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels, const uint8_t* rep,
+                      const mvs_array* a, const mvs_refine_params* p, float* state_out, float* disp) {
+  if (!c || !spixl || !labels || !rep || !p || S <= 0 || bad_dims(W, H)) return mvs::arg_fail("mvs_do_refinement: bad arguments");
+  RC(check_array(a));
+  int V = a->view_count;
+  size_t P = (size_t)W * H;
+  int mw = mvs::map_dim(W, S), mh = mvs::map_dim(H, S);
+  size_t M = (size_t)mw * mh;
+  DevBuf dsp, dlb, drep, dfl, dst, dst2, ddisp;
+  RC(dsp.alloc(V * M * 32));
+  RC(dlb.alloc(V * P * 4));
+  RC(drep.alloc(V * M * 8));
+  RC(dfl.alloc(V * M * 8));
+  RC(dst.alloc(V * M * 24));
+  RC(dst2.alloc(V * M * 24));
+  RC(ddisp.alloc(V * P * 4));
+  hipStream_t s = c->stream;
+  MVS_HIP(hipMemcpyAsync(dsp.p, spixl, V * M * 32, hipMemcpyHostToDevice, s), "H2D spixl");
+  MVS_HIP(hipMemcpyAsync(dlb.p, labels, V * P * 4, hipMemcpyHostToDevice, s), "H2D labels");
+  MVS_HIP(hipMemcpyAsync(drep.p, rep, V * M * 8, hipMemcpyHostToDevice, s), "H2D rep");
+  RC(mvs_refine_d(c, W, H, S, dsp.as<float>(), dlb.as<uint32_t>(), drep.as<uint8_t>(), a, p, dfl.as<float>(),
+                  dst.as<float>(), dst2.as<float>(), disp ? ddisp.as<float>() : nullptr));
+  if (state_out) {
+    const void* src = dst.p;
+    if (!p->fusion_compat && p->no_prop > 0) src = ((p->no_prop - 1) % 2 == 0) ? dst2.p : dst.p;
+    MVS_HIP(hipMemcpyAsync(state_out, src, V * M * 24, hipMemcpyDeviceToHost, s), "D2H state");
+  }
+  if (disp) MVS_HIP(hipMemcpyAsync(disp, ddisp.p, V * P * 4, hipMemcpyDeviceToHost, s), "D2H disp");
+  MVS_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
+}  // extern "C"

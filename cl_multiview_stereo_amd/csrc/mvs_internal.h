@@ -1,0 +1,94 @@
+// Internal helpers shared by the HIP translation units of libmvs.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/mvs.h"
+#include "../../include/mvs_detmath.h"
+
+struct mvs_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  // persistent scratch (grown on demand)
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  // device copy of the last mvs_array metadata
+  float* d_levels = nullptr;
+  int* d_vs = nullptr;
+  int* d_sn = nullptr;
+  size_t cap_levels = 0, cap_vs = 0, cap_sn = 0;
+  std::vector<float> h_levels;
+  std::vector<int> h_vs, h_sn;
+};
+
+namespace mvs {
+
+void set_error(const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+int arg_fail(const char* what);
+void* scratch(mvs_ctx* ctx, size_t bytes, int* rc);
+
+inline int map_dim(int n, int S) {
+  // (int)ceil((float)n / (float)S), pipeline.cpp:18-19
+  return (int)__builtin_ceilf((float)n / (float)S);
+}
+
+constexpr int kLocal = 16;  // LOCAL_SIZE_UPDATE, header.h:37-38
+
+#define MVS_LAUNCH_CHECK(what)                          \
+  do {                                                  \
+    hipError_t _e = hipGetLastError();                  \
+    if (_e != hipSuccess) return mvs::hip_fail(_e, what); \
+  } while (0)
+
+#define MVS_HIP(call, what)                              \
+  do {                                                   \
+    hipError_t _e = (call);                              \
+    if (_e != hipSuccess) return mvs::hip_fail(_e, what); \
+  } while (0)
+
+// ---- launchers implemented in the .hip files (device pointers) ------------
+int launch_cvt(hipStream_t s, const uint8_t* rgbx, long npix, float* lab, uint8_t* l8);
+int launch_init_centers(hipStream_t s, const float* lab, int V, int W, int H, int S, float* spixl);
+int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labels);
+int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
+                  float col_n, float weight, uint32_t* labels);
+int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V, int W, int H, int S,
+                  float* spixl);
+int launch_suppress(hipStream_t s, const uint32_t* in, uint32_t* out, int V, int W, int H);
+
+int launch_boundary(hipStream_t s, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                    uint8_t* rep);
+int launch_sweep_spixl(hipStream_t s, int V, int W, int H, int S, const float* lab, float* spixl,
+                       const uint8_t* rep, const float* levels, int D, const int* vs, const int* sn, int aw,
+                       float bl, int z0, int z1);
+int launch_sweep_pixel_sad(hipStream_t s, int V, int W, int H, const float* lab, const float* levels, int D,
+                           const int* vs, const int* sn, const int* sn_host, int aw, float bl, int z0, int z1,
+                           float* disp);
+int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box);
+int launch_ncc_volume(hipStream_t s, int V, int W, int H, const uint8_t* l8, const int32_t* box,
+                      const float* levels_host, int D, const int* vs_host, const int* sn_host, int aw, float bl,
+                      int K, int z, float* vol);
+int launch_wta(hipStream_t s, int W, int H, int D, const float* vol, const float* levels, float* disp,
+               float* conf);
+
+int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat);
+int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
+                      const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                      const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state);
+int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
+                     const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                     const int* sn, int iter, float alpha, float gamma, float fuse, int nks, float kss,
+                     const float* st_in, float* st_out, int z0, int z1);
+int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float* spixl,
+                          const uint32_t* labels, const float* state, float* disp);
+int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
+                  float* proj, float* out, int z0, int z1);
+
+}  // namespace mvs

@@ -1,0 +1,489 @@
+// Superpixel-plane refinement + fusion + cross-view filter for gfx950.
+//
+//  k_flatness        compute_flatness          clcode.cl:1076-1132
+//  k_init_state      init_current_state        clcode.cl:1136-1404
+//  k_propagate       propagate (+update, spatialRefinement, compute_smoothness,
+//                    compute_consistency)       clcode.cl:1407-1900
+//  k_spixl_to_image  spixl_to_image            clcode.cl:1906-1931
+//  k_proj_inv /      project_to_reference_inv / remove_view_inconsistency
+//  k_remove_incons   clcode.cl:1995-2101 (pinned order)
+//
+// Refinement is a latency-bound gather workload: one lane per
+// (superpixel, view), candidate plane evaluations in the reference's order.
+// The per-superpixel inputs are packed once per launch into 32-B records so a
+// gather touches one cache line.  Numerics follow include/mvs_detmath.h.
+#include "mvs_internal.h"
+
+namespace mvs {
+namespace {
+
+struct RArgs {
+  int V, W, H, S, mw, mh, aw;
+  float bl, fuse, alpha, gamma;
+};
+
+__device__ __forceinline__ float expf_neg_sq(float diff, float k) { return mvs_expf(((-diff) * diff) * k); }
+
+__device__ __forceinline__ float plane_at(float nx, float ny, float nz, float cx, float cy, float d, float px,
+                                          float py) {
+  float t = nx * (cx - px);
+  t = t + ny * (cy - py);
+  t = t + nz * d;
+  return t / nz;
+}
+
+__device__ __forceinline__ int step_size_of(float flx, float kss) {
+  int s = (int)((double)(flx * kss) + 0.5);
+  return s > 1 ? s : 1;
+}
+
+// ---- compute_flatness ------------------------------------------------------
+__global__ void k_flatness(const float* __restrict__ spixl, int mw, int mh, float gamma, float2* __restrict__ flat) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= mw) return;
+  long M = (long)mw * mh;
+  long idx = M * z + (long)mw * y + x;
+  const float* c0 = spixl + 8 * idx + 3;
+  float fl = 1.0f;
+  long nb[4] = {idx - 1, idx + 1, idx + mw, idx - mw};
+  bool ok[4] = {x - 1 >= 0, x + 1 < mw, y + 1 < mh, y - 1 >= 0};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (!ok[k]) continue;
+    const float* c1 = spixl + 8 * nb[k] + 3;
+    float diff = (c1[0] - c0[0]) * (c1[0] - c0[0]);
+    diff = diff + (c1[1] - c0[1]) * (c1[1] - c0[1]);
+    diff = diff + (c1[2] - c0[2]) * (c1[2] - c0[2]);
+    fl = fl + diff;
+  }
+  flat[idx] = make_float2(mvs_expf((-fl) * gamma), (float)(1.0 - mvs_exp((-0.25 * (double)fl) * (double)gamma)));
+}
+
+// ---- init_smoothness + initialize_consistency + init_current_state ---------
+__device__ float init_smoothness(const RArgs& c, const float* __restrict__ spixl, const float* sp, float2 fl, int x,
+                                 int y, int z, int nks, float kss) {
+  long M = (long)c.mw * c.mh;
+  float sm = 0.0f, wn = 0.0f;
+  float cl0 = sp[3], cl1 = sp[4], cl2 = sp[5], disp = sp[7];
+  for (int i = -1; i <= 1; i++)
+    for (int j = -1; j <= 1; j++) {
+      int px = x + i, py = y + j;
+      if (px >= 0 && py >= 0 && px < c.mw && py < c.mh && (i != 0 || j != 0)) {
+        const float* s = spixl + 8 * (M * z + (long)c.mw * py + px);
+        float diff = mvs_distance3(s[3], s[4], s[5], cl0, cl1, cl2);
+        float simi = expf_neg_sq(diff, c.gamma);
+        diff = disp - s[7];
+        sm = sm + simi * expf_neg_sq(diff, c.alpha);
+        wn = wn + simi;
+      }
+    }
+  int ss = step_size_of(fl.x, kss);
+  for (int i = 1; i <= nks; i++) {
+    float gi = c.gamma * (float)(1 + i);
+    int step = i * ss;
+    int cx[4] = {x - (step + 1), x + (step + 1), x, x};
+    int cy[4] = {y, y, y - step - 1, y + step + 1};
+    bool ok[4] = {x > step, x < c.mw - step - 1, y > step, y < c.mh - step - 1};
+    for (int k = 0; k < 4; k++) {
+      if (!ok[k]) continue;
+      const float* s = spixl + 8 * (M * z + (long)c.mw * cy[k] + cx[k]);
+      float diff = mvs_distance3(cl0, cl1, cl2, s[3], s[4], s[5]);
+      float simi = expf_neg_sq(diff, gi);
+      diff = disp - s[7];
+      sm = sm + simi * expf_neg_sq(diff, c.alpha);
+      wn = wn + simi;
+    }
+  }
+  return wn > 0 ? sm / wn : 0.000001f;
+}
+
+__device__ __forceinline__ void samples_of(const uint8_t* r, int* s) {
+  s[0] = r[0]; s[1] = r[1]; s[2] = r[2]; s[3] = r[3]; s[4] = 0;
+  s[5] = r[4]; s[6] = r[5]; s[7] = r[6]; s[8] = r[7];
+}
+
+__device__ __forceinline__ float finish_consistency(float cons, int vc) {
+  float margin = 0.01f;
+  return vc > 0 ? fmaxf(margin, cons / (float)vc) : margin;
+}
+
+__device__ float init_consistency(const RArgs& c, const float* __restrict__ spixl, const uint32_t* __restrict__ labels,
+                                  const uint8_t* rp, const int* __restrict__ vs, const int* __restrict__ sn, int z,
+                                  const float* color, float cxf, float cyf, float d, float2 fl) {
+  long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
+  float cons = 0.0f;
+  int vc = 0;
+  int camx = z % c.aw, camy = z / c.aw;
+  int smp[9];
+  samples_of(rp, smp);
+  for (int n = 0; n < sn[z]; n++) {
+    int view = vs[z * c.V + n];
+    int vx = view % c.aw, vy = view / c.aw;
+    float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
+    for (int i = -1; i <= 1; i++)
+      for (int j = -1; j <= 1; j++) {
+        int xr = (int)cxf + smp[(i + 1) * 3 + j + 1] * i;
+        int yr = (int)cyf + smp[(i + 1) * 3 + j + 1] * j;
+        int xp = (int)((float)xr - roundf(d * (float)(vx - camx)));
+        int yp = (int)((float)yr - roundf((c.bl * d) * (float)(vy - camy)));
+        if (xp >= 0 && yp >= 0 && xp < c.W && yp < c.H) {
+          uint32_t ip = labels[P * view + (long)c.W * yp + xp];
+          uint32_t sx = ip % (uint32_t)c.mw, sy = ip / (uint32_t)c.mw;
+          const float* s = spixl + 8 * (M * view + (long)c.mw * sy + sx);
+          float diff = s[7] - d;
+          float wv = fabsf(diff) < c.fuse ? 1.0f : 0.0f;
+          visible = visible + wv * expf_neg_sq(diff, c.alpha);
+          vis_w = vis_w + wv;
+          occ_w = occ_w + (1.0f - wv);
+          diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+          visibility = visibility + expf_neg_sq(diff, c.gamma);
+          num = num + 1.0f;
+        }
+      }
+    if (num > 0) {
+      vc++;
+      if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+      if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)fl.y);
+    }
+  }
+  return finish_consistency(cons, vc);
+}
+
+__global__ __launch_bounds__(256) void k_init_state(RArgs c, const float* __restrict__ spixl,
+                                                    const uint32_t* __restrict__ labels,
+                                                    const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
+                                                    const int* __restrict__ vs, const int* __restrict__ sn, int nks,
+                                                    float kss, float* __restrict__ state) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= c.mw) return;
+  long M = (long)c.mw * c.mh;
+  long idx = M * z + (long)c.mw * y + x;
+  const float* sp = spixl + 8 * idx;
+  float2 fl = flat[idx];
+  float sm = init_smoothness(c, spixl, sp, fl, x, y, z, nks, kss);
+  float color[3] = {sp[3], sp[4], sp[5]};
+  float cs = init_consistency(c, spixl, labels, rep + 8 * idx, vs, sn, z, color, sp[1], sp[2], sp[7], fl);
+  float* o = state + 6 * idx;
+  o[0] = sp[7]; o[1] = sm; o[2] = cs; o[3] = 0.0f; o[4] = 0.0f; o[5] = 1.0f;
+}
+
+// ---- propagate -------------------------------------------------------------
+struct PState {
+  float d, sm, cs, nx, ny, nz;
+};
+
+struct PCtx {
+  RArgs c;
+  const float* spixl;
+  const uint32_t* labels;
+  const int* vs;
+  const int* sn;
+  const float* st;
+  int smp[9];
+  int x, y, z, iter, nks;
+  float kss;
+  float cx, cy, col[3];
+  float2 fl;
+};
+
+__device__ float comp_smoothness(const PCtx& p, float d, float nx, float ny, float nz) {
+  const RArgs& c = p.c;
+  long M = (long)c.mw * c.mh;
+  float sm = 0.0f, wn = 0.0f;
+  for (int i = -1; i <= 1; i++)
+    for (int j = -1; j <= 1; j++) {
+      int px = p.x + i, py = p.y + j;
+      if (px >= 0 && py >= 0 && px < c.mw && py < c.mh && (i != 0 || j != 0)) {
+        long q = M * p.z + (long)c.mw * py + px;
+        const float* s = p.spixl + 8 * q;
+        float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], s[3], s[4], s[5]);
+        float simi = expf_neg_sq(diff, c.gamma);
+        float di = plane_at(nx, ny, nz, p.cx, p.cy, d, s[1], s[2]);
+        diff = di - p.st[6 * q];
+        sm = sm + simi * expf_neg_sq(diff, c.alpha);
+        wn = wn + simi;
+      }
+    }
+  int ss = step_size_of(p.fl.x, p.kss);
+  for (int i = 1; i <= p.nks; i++) {
+    float gi = c.gamma * (float)(1 + i);
+    int step = i * ss;
+    int cxs[4] = {p.x - (step + 1), p.x + (step + 1), p.x, p.x};
+    int cys[4] = {p.y, p.y, p.y - (step + 1), p.y + (step + 1)};
+    bool ok[4] = {p.x > step, p.x < c.mw - step - 1, p.y > step, p.y < c.mh - step - 1};
+    for (int k = 0; k < 4; k++) {
+      if (!ok[k]) continue;
+      long q = M * p.z + (long)c.mw * cys[k] + cxs[k];
+      const float* s = p.spixl + 8 * q;
+      float diff = mvs_distance3(s[3], s[4], s[5], p.col[0], p.col[1], p.col[2]);
+      float simi = expf_neg_sq(diff, gi);
+      float de = plane_at(nx, ny, nz, p.cx, p.cy, d, s[1], s[2]);
+      diff = de - p.st[6 * q];
+      sm = sm + simi * expf_neg_sq(diff, c.alpha);
+      wn = wn + simi;
+    }
+  }
+  return wn > 0 ? sm / wn : 0.000001f;
+}
+
+__device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, float nz) {
+  const RArgs& c = p.c;
+  long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
+  float cons = 0.0f;
+  int vc = 0;
+  int camx = p.z % c.aw, camy = p.z / c.aw;
+  for (int k = 0; k < p.sn[p.z]; k++) {
+    int view = p.vs[c.V * p.z + k];
+    float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
+    int vx = view % c.aw, vy = view / c.aw;
+    for (int i = -1; i <= 1; i++)
+      for (int j = -1; j <= 1; j++) {
+        int sx = (int)p.cx + p.smp[(i + 1) * 3 + j + 1] * i;
+        int sy = (int)p.cy + p.smp[(i + 1) * 3 + j + 1] * j;
+        float di = plane_at(nx, ny, nz, p.cx, p.cy, d, (float)sx, (float)sy);
+        int xp = (int)((float)sx - roundf(di * (float)(vx - camx)));
+        int yp = (int)((float)sy - roundf((c.bl * di) * (float)(vy - camy)));
+        if (xp >= 0 && yp >= 0 && xp < c.W && yp < c.H) {
+          uint32_t ip = p.labels[P * view + (long)c.W * yp + xp];
+          uint32_t qx = ip % (uint32_t)c.mw, qy = ip / (uint32_t)c.mw;
+          long q = M * view + (long)c.mw * qy + qx;
+          const float* s = p.spixl + 8 * q;
+          const float* sq = p.st + 6 * q;
+          float dip = plane_at(sq[3], sq[4], sq[5], s[1], s[2], sq[0], (float)xp, (float)yp);
+          float diff = dip - di;
+          float wv = fabsf(diff) < c.fuse ? 1.0f : 0.0f;
+          visible = visible + wv * expf_neg_sq(diff, c.alpha);
+          vis_w = vis_w + wv;
+          occ_w = occ_w + (1.0f - wv);
+          diff = mvs_distance3(s[3], s[4], s[5], p.col[0], p.col[1], p.col[2]);
+          visibility = visibility + expf_neg_sq(diff, c.gamma);
+          num = num + 1.0f;
+        }
+      }
+    if (num > 0) {
+      vc++;
+      if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+      if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)p.fl.y);
+    }
+  }
+  return finish_consistency(cons, vc);
+}
+
+// update, clcode.cl:1635-1673
+__device__ void plane_update(const PCtx& p, long q, PState& cur) {
+  const float* s1 = p.st + 6 * q;
+  float nx = s1[3], ny = s1[4], nz = s1[5], d1 = s1[0];
+  const float* sc = p.spixl + 8 * q;
+  float t = nx * (sc[1] - p.cx);
+  t = t + ny * (sc[2] - p.cy);
+  t = t + nz * d1;
+  float di = t / nz;
+  float sm1 = comp_smoothness(p, di, nx, ny, nz);
+  float cs1 = comp_consistency(p, di, nx, ny, nz);
+  float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], sc[3], sc[4], sc[5]);
+  float simi = expf_neg_sq(diff, p.c.gamma);
+  if ((p.iter < 4 && sm1 * simi > cur.sm) || cs1 * sm1 > cur.sm * cur.cs) {
+    cur.d = di; cur.sm = sm1; cur.cs = cs1; cur.nx = nx; cur.ny = ny; cur.nz = nz;
+  }
+}
+
+// spatialRefinement + cross_product_test + normalize, clcode.cl:1676-1723
+__device__ void spatial_refine(const PCtx& p, int ax, int ay, int bx, int by, PState& cur) {
+  const RArgs& c = p.c;
+  long M = (long)c.mw * c.mh;
+  long q1 = M * p.z + (long)c.mw * ay + ax, q2 = M * p.z + (long)c.mw * by + bx;
+  const float* a1 = p.spixl + 8 * q1;
+  const float* a2 = p.spixl + 8 * q2;
+  float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = p.st[6 * q1] - cur.d;
+  float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = p.st[6 * q2] - cur.d;
+  float n0 = v1y * v2z - v1z * v2y;
+  float n1 = v2x * v1z - v1x * v2z;
+  float n2 = v1x * v2y - v1y * v2x;
+  float n3 = 0.0f;
+  float s = n0 * n0;
+  s = s + n1 * n1;
+  s = s + n2 * n2;
+  s = s + n3 * n3;
+  if (s != 0.0f) {
+    float r = sqrtf(s);
+    n0 = n0 / r; n1 = n1 / r; n2 = n2 / r;
+  }
+  float sm1 = comp_smoothness(p, cur.d, n0, n1, n2);
+  float cs1 = comp_consistency(p, cur.d, n0, n1, n2);
+  if ((p.iter < 4 && sm1 > cur.sm) || sm1 * cs1 > cur.sm * cur.cs) {
+    cur.sm = sm1; cur.cs = cs1; cur.nx = n0; cur.ny = n1; cur.nz = n2;
+  }
+}
+
+__global__ __launch_bounds__(128) void k_propagate(RArgs c, const float* __restrict__ spixl,
+                                                   const uint32_t* __restrict__ labels,
+                                                   const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
+                                                   const int* __restrict__ vs, const int* __restrict__ sn, int iter,
+                                                   int nks, float kss, const float* __restrict__ st_in,
+                                                   float* __restrict__ st_out, int z0) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = z0 + blockIdx.z;
+  if (x >= c.mw) return;
+  long M = (long)c.mw * c.mh;
+  long idx = M * z + (long)c.mw * y + x;
+  PCtx p;
+  p.c = c; p.spixl = spixl; p.labels = labels; p.vs = vs; p.sn = sn; p.st = st_in;
+  p.x = x; p.y = y; p.z = z; p.iter = iter; p.nks = nks; p.kss = kss;
+  const float* sp = spixl + 8 * idx;
+  p.cx = sp[1]; p.cy = sp[2]; p.col[0] = sp[3]; p.col[1] = sp[4]; p.col[2] = sp[5];
+  p.fl = flat[idx];
+  samples_of(rep + 8 * idx, p.smp);
+  const float* si = st_in + 6 * idx;
+  PState cur{si[0], si[1], si[2], si[3], si[4], si[5]};
+  for (int i = -1; i <= 1; i++)
+    for (int j = -1; j <= 1; j++) {
+      int px = x + i, py = y + j;
+      if (px >= 0 && py >= 0 && px < c.mw && py < c.mh && !(i == 0 && j == 0))
+        plane_update(p, M * z + (long)c.mw * py + px, cur);
+    }
+  int ssz = (int)kss;
+  for (int i = 1; i <= nks; i++) {
+    int off = i * ssz;
+    if (y > off) plane_update(p, M * z + (long)c.mw * (y - (off + 1)) + x, cur);
+    if (y < c.mh - off - 1) plane_update(p, M * z + (long)c.mw * (y + off + 1) + x, cur);
+    if (x > off) plane_update(p, M * z + (long)c.mw * y + (x - off - 1), cur);
+    if (x < c.mw - off - 1) plane_update(p, M * z + (long)c.mw * y + (x + off + 1), cur);
+  }
+  const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
+  const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
+  for (int i = 0; i < 8; i++) {
+    int j = (i + 1) % 8;
+    if (nbx[i] > -1 && nby[i] > -1 && nbx[i] < c.mw && nby[i] < c.mh && nbx[j] > -1 && nby[j] > -1 &&
+        nbx[j] < c.mw && nby[j] < c.mh)
+      spatial_refine(p, nbx[i], nby[i], nbx[j], nby[j], cur);
+  }
+  float* o = st_out + 6 * idx;
+  o[0] = cur.d; o[1] = cur.sm; o[2] = cur.cs; o[3] = cur.nx; o[4] = cur.ny; o[5] = cur.nz;
+}
+
+// ---- spixl_to_image ----------------------------------------------------------
+__global__ void k_spixl_to_image(const float* __restrict__ spixl, const uint32_t* __restrict__ labels,
+                                 const float* __restrict__ st, int W, int H, int mw, int mh,
+                                 float* __restrict__ disp) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= W) return;
+  long M = (long)mw * mh, P = (long)W * H;
+  int id = (int)labels[P * z + (long)W * y + x];
+  int sx = id % mw, sy = id / mw;
+  long q = M * z + (long)mw * sy + sx;
+  const float* s = spixl + 8 * q;
+  const float* t = st + 6 * q;
+  float v = t[3] * (s[1] - (float)x);
+  v = v + t[4] * (s[2] - (float)y);
+  v = v + t[5] * t[0];
+  disp[P * z + (long)W * y + x] = v / t[5];
+}
+
+// ---- cross-view filter -------------------------------------------------------
+__global__ void k_proj_inv(const float* __restrict__ full, int V, int W, int H, int aw, float bl,
+                           float* __restrict__ proj) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = blockIdx.z;
+  if (x >= W) return;
+  long P = (long)W * H, p = (long)y * W + x;
+  int crx = r % aw, cry = r / aw;
+  float md = full[P * r + p];
+  for (int i = 0; i < V; i++) {
+    if (i == r) continue;
+    int cx = i % aw, cy = i / aw;
+    int xp = (int)((float)x - roundf(md * (float)(crx - cx)));
+    int yp = (int)((float)y - roundf((bl * md) * (float)(cry - cy)));
+    if (xp >= 0 && yp >= 0 && xp < W && yp < H) {
+      float cd = full[P * i + (long)W * yp + xp];
+      if (md < cd) md = cd;
+    }
+  }
+  proj[P * r + p] = md;
+}
+
+__global__ void k_remove_incons(const float* __restrict__ proj, const float* __restrict__ full, int V, int W, int H,
+                                int aw, float bl, float fuse, int z0, float* __restrict__ out) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
+  if (x >= W) return;
+  long P = (long)W * H, p = (long)y * W + x;
+  int crx = r % aw, cry = r / aw;
+  float dest = 0.0f;
+  for (int i = 0; i < V; i++) {
+    float d = proj[P * i + p];
+    if (d != 0) {
+      float stab = 0.0f;
+      for (int j = 0; j < V; j++) {
+        float dc = proj[P * j + p];
+        if (dc != 0) {
+          float diff = dc - d;
+          if (fabsf(diff) > fuse) stab = stab - 1.0f;
+          if (fabsf(diff) <= fuse) stab = stab + 1.0f;
+        }
+      }
+      for (int j = 0; j < V; j++) {
+        int cx = j % aw, cy = j / aw;
+        int xx = (int)((float)x - roundf(d * (float)(cx - crx)));
+        int yy = (int)((float)y - roundf((bl * d) * (float)(cy - cry)));
+        if (xx >= 0 && yy >= 0 && xx < W && yy < H) {
+          float dc = full[P * j + (long)W * yy + xx];
+          float diff = dc - d;
+          if (fabsf(diff) > fuse) stab = stab - 1.0f;
+          if (fabsf(diff) < fuse) stab = stab + 1.0f;
+        }
+      }
+      if (stab >= 0 && (dest == 0 || dest < d)) dest = d;
+    }
+  }
+  out[P * r + p] = dest;
+}
+
+}  // namespace
+
+int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
+  hipLaunchKernelGGL(k_flatness, dim3((mw + 63) / 64, mh, V), dim3(64), 0, s, spixl, mw, mh, gamma, (float2*)flat);
+  MVS_LAUNCH_CHECK("k_flatness");
+  return 0;
+}
+
+int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
+                      const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                      const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state) {
+  RArgs c{V, W, H, S, map_dim(W, S), map_dim(H, S), aw, bl, fuse, alpha, gamma};
+  hipLaunchKernelGGL(k_init_state, dim3((c.mw + 63) / 64, c.mh, V), dim3(64), 0, s, c, spixl, labels, rep,
+                     (const float2*)flat, vs, sn, nks, kss, state);
+  MVS_LAUNCH_CHECK("k_init_state");
+  return 0;
+}
+
+int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
+                     const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                     const int* sn, int iter, float alpha, float gamma, float fuse, int nks, float kss,
+                     const float* st_in, float* st_out, int z0, int z1) {
+  if (z1 <= z0) return 0;
+  RArgs c{V, W, H, S, map_dim(W, S), map_dim(H, S), aw, bl, fuse, alpha, gamma};
+  hipLaunchKernelGGL(k_propagate, dim3((c.mw + 63) / 64, c.mh, z1 - z0), dim3(64), 0, s, c, spixl, labels, rep,
+                     (const float2*)flat, vs, sn, iter, nks, kss, st_in, st_out, z0);
+  MVS_LAUNCH_CHECK("k_propagate");
+  return 0;
+}
+
+int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                          const float* state, float* disp) {
+  int mw = map_dim(W, S), mh = map_dim(H, S);
+  hipLaunchKernelGGL(k_spixl_to_image, dim3((W + 255) / 256, H, V), dim3(256), 0, s, spixl, labels, state, W, H,
+                     mw, mh, disp);
+  MVS_LAUNCH_CHECK("k_spixl_to_image");
+  return 0;
+}
+
+int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
+                  float* proj, float* out, int z0, int z1) {
+  hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, H, V), dim3(256), 0, s, full, V, W, H, aw, bl, proj);
+  MVS_LAUNCH_CHECK("k_proj_inv");
+  if (z1 > z0) {
+    hipLaunchKernelGGL(k_remove_incons, dim3((W + 255) / 256, H, z1 - z0), dim3(256), 0, s, proj, full, V, W, H,
+                       aw, bl, fuse, z0, out);
+    MVS_LAUNCH_CHECK("k_remove_incons");
+  }
+  return 0;
+}
+
+}  // namespace mvs

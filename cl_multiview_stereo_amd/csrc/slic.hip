@@ -1,0 +1,280 @@
+// SLIC superpixel kernels for gfx950 (CDNA4, wave64).
+//
+// Semantics restate clMVDE/clcode.cl (file:line at each kernel) under the
+// numerical definition of include/mvs_detmath.h; layouts are the reference's.
+// Design: pixel kernels are HBM-streaming (one lane per pixel, 16-B Lab
+// loads/stores); the centre update is one workgroup per superpixel that walks
+// the reference's 16x16 window tiles with one wave per tile and reproduces the
+// reference LDS tree (stride 128..1) with two in-lane steps + six cross-lane
+// shuffles, then sums the tile partials in tile order in the same workgroup
+// (update_cluster_center and finalize_reduction_result fused: no accum_map
+// round trip through HBM).
+#include "mvs_internal.h"
+
+namespace mvs {
+namespace {
+
+// ---- rgb2lab + cvt, clcode.cl:21-59, 125-151 (s0 read as blue) -----------
+__device__ __forceinline__ float4 rgb2lab(uint32_t px) {
+  float _b = (float)(px & 0xffu) * 0.0039216f;
+  float _g = (float)((px >> 8) & 0xffu) * 0.0039216f;
+  float _r = (float)((px >> 16) & 0xffu) * 0.0039216f;
+  float x = _r * 0.412453f + _g * 0.357580f + _b * 0.180423f;
+  float y = _r * 0.212671f + _g * 0.715160f + _b * 0.072169f;
+  float z = _r * 0.019334f + _g * 0.119193f + _b * 0.950227f;
+  const float epsilon = 0.008856f, kappa = 903.3f;
+  float xr = x / 0.950456f, yr = y / 1.0f, zr = z / 1.088754f;
+  const float third = 1.0f / 3.0f;
+  float fx = xr > epsilon ? mvs_powrf(xr, third) : (kappa * xr + 16.0f) / 116.0f;
+  float fy = yr > epsilon ? mvs_powrf(yr, third) : (kappa * yr + 16.0f) / 116.0f;
+  float fz = zr > epsilon ? mvs_powrf(zr, third) : (kappa * zr + 16.0f) / 116.0f;
+  return make_float4(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz), 0.0f);
+}
+
+__global__ __launch_bounds__(256) void k_cvt(const uint32_t* __restrict__ rgbx, long n, float4* __restrict__ lab,
+                                             uint8_t* __restrict__ l8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float4 v = rgb2lab(__builtin_nontemporal_load(rgbx + i));
+    lab[i] = v;
+    if (l8) {
+      // build-defined NCC intensity: clamp((int)(L*2.55f + 0.5f), 0, 255)
+      float t = v.x * 2.55f;
+      t = t + 0.5f;
+      int q = (int)t;
+      l8[i] = (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+    }
+  }
+}
+
+// ---- init_cluster_centers, clcode.cl:259-294 -----------------------------
+__global__ void k_init_centers(const float4* __restrict__ lab, int W, int H, int S, int mw, int mh,
+                               float* __restrict__ spixl) {
+  int col = blockIdx.x * blockDim.x + threadIdx.x, row = blockIdx.y, z = blockIdx.z;
+  if (col >= mw || row >= mh) return;
+  int ci = row * mw + col;
+  int cx = col * S + S / 2, cy = row * S + S / 2;
+  if (cx > W) cx = (col * S + W) / 2;
+  if (cy > H) cy = (row * S + H) / 2;
+  long P = (long)W * H;
+  float* o = spixl + 8 * ((long)z * mw * mh + ci);
+  o[0] = (float)ci;
+  o[1] = (float)cx;
+  o[2] = (float)cy;
+  long p = (long)cy * W + cx;  // cx == W reads the next row (reference); past the end pinned to 0
+  float4 c = p < P ? lab[(long)z * P + p] : make_float4(0.f, 0.f, 0.f, 0.f);
+  o[3] = c.x;
+  o[4] = c.y;
+  o[5] = c.z;
+  o[6] = 0.0f;
+}
+
+// ---- init_label_per_pixl, clcode.cl:341-353 ------------------------------
+__global__ void k_grid_labels(int W, int H, int S, int mw, uint32_t* __restrict__ labels) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= W) return;
+  labels[((long)z * H + y) * W + x] = (uint32_t)(mw * (y / S) + x / S);
+}
+
+// ---- slic_distance_function + find_center_association, clcode.cl:422-520 -
+__device__ __forceinline__ float slic_dist(float4 px, int y, int x, const float* c, float weight, float sn,
+                                           float cn) {
+  float a = (px.x - c[3]) * (px.x - c[3]);
+  a = a + (px.y - c[4]) * (px.y - c[4]);
+  a = a + (px.z - c[5]) * (px.z - c[5]);
+  float b = ((float)x - c[1]) * ((float)x - c[1]);
+  b = b + ((float)y - c[2]) * ((float)y - c[2]);
+  float d = (a * cn) + weight * (b * sn);
+  return sqrtf(d);
+}
+
+__global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, const float* __restrict__ spixl,
+                                                int W, int H, int S, int mw, int mh, float xy_n, float col_n,
+                                                float weight, uint32_t* __restrict__ labels) {
+  int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  int row = blockIdx.y * 4 + (threadIdx.x >> 6);
+  int z = blockIdx.z;
+  if (col >= W || row >= H) return;
+  long P = (long)W * H;
+  long pid = (long)z * P + (long)row * W + col;
+  const float* sp = spixl + 8L * z * mw * mh;
+  float4 px = lab[pid];
+  int cxg = col / S, cyg = row / S;
+  int dX = (col + S / 2) / S - cxg, dY = (row + S / 2) / S - cyg;
+  float min_dist = 999999.9999f, min_id = -1.0f;
+  for (int i = -1 + dX; i <= dX; i++)      // i spans the x delta but offsets y
+    for (int j = -1 + dY; j <= dY; j++) {  // (Appendix A #2, reproduced)
+      int cx = cxg + j, cy = cyg + i;
+      if (cx >= 0 && cy >= 0 && cx < mw && cy < mh) {
+        int ci = cy * mw + cx;
+        float d = slic_dist(px, row, col, sp + 8 * ci, weight, xy_n, col_n);
+        if (d < min_dist) {
+          min_dist = d;
+          min_id = (float)ci;
+        }
+      }
+    }
+  labels[pid] = (uint32_t)min_id;
+}
+
+// ---- update_cluster_center + finalize_reduction_result -------------------
+// clcode.cl:533-611 (per-tile LDS tree) and 719-773 (in-order partial sum),
+// launch shape clSLIC.cpp:307-370.  One workgroup per (superpixel, view).
+__device__ __forceinline__ float wave_tree(float v0, float v1, float v2, float v3) {
+  // local_idx k = lane + 64*m holds v_m.  stride 128: k<128 gets k+128; stride
+  // 64: k<64 gets k+64; strides 32..1 stay inside the wave.
+  float s = (v0 + v2) + (v1 + v3);
+#pragma unroll
+  for (int i = 32; i >= 1; i >>= 1) s = s + __shfl_down(s, (unsigned)i, 64);
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, const uint32_t* __restrict__ labels,
+                                                int W, int H, int S, int mw, int mh, int G, int cpl,
+                                                float* __restrict__ spixl) {
+  extern __shared__ float part[];  // [G][6]
+  int sp = blockIdx.x, z = blockIdx.y;
+  int gx = sp % mw, gy = sp / mw;
+  long P = (long)W * H;
+  const float4* L = lab + (long)z * P;
+  const uint32_t* I = labels + (long)z * P;
+  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int lx = lane & 15, ly0 = lane >> 4;
+  for (int t = wave; t < G; t += 4) {
+    int nbx = t % cpl, nby = t / cpl;
+    float v[4][6];
+    bool any = false;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      int ly = ly0 + 4 * m;
+      int pxo = nbx * kLocal + lx, pyo = nby * kLocal + ly;
+      int px = gx * S - S + pxo, py = gy * S - S + pyo;
+      bool in = pyo < S * 3 && pxo < S * 3 && py >= 0 && px >= 0 && px < W && py < H;
+      bool mem = false;
+      if (in) mem = I[(long)py * W + px] == (uint32_t)sp;
+      float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (mem) c = L[(long)py * W + px];
+      v[m][0] = mem ? (float)px : 0.0f;
+      v[m][1] = mem ? (float)py : 0.0f;
+      v[m][2] = c.x;
+      v[m][3] = c.y;
+      v[m][4] = c.z;
+      v[m][5] = mem ? 1.0f : 0.0f;
+      any |= mem;
+    }
+    float r[6];
+    if (__any(any)) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) r[c] = wave_tree(v[0][c], v[1][c], v[2][c], v[3][c]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 6; c++) r[c] = 0.0f;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) part[t * 6 + c] = r[c];
+    }
+  }
+  __syncthreads();
+  __shared__ float acc[6];
+  if (threadIdx.x < 6) {
+    float a = 0.0f;
+    for (int t = 0; t < G; t++) a = a + part[t * 6 + threadIdx.x];
+    acc[threadIdx.x] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float* o = spixl + 8 * ((long)z * mw * mh + sp);
+    float n = acc[5];
+    o[0] = (float)sp;
+    if (n != 0) {
+      o[1] = acc[0] / n;
+      o[2] = acc[1] / n;
+      o[3] = acc[2] / n;
+      o[4] = acc[3] / n;
+      o[5] = acc[4] / n;
+      o[6] = n;
+    } else {
+      o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
+    }
+  }
+}
+
+// ---- supress_local_lable, clcode.cl:676-711 ------------------------------
+__global__ void k_suppress(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, int W, int H) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= W) return;
+  long base = (long)z * W * H;
+  long idx = base + (long)y * W + x;
+  int cl = (int)in[idx];
+  if (x <= 1 || y <= 1 || x >= W - 2 || y >= H - 2) {
+    out[idx] = (uint32_t)cl;
+    return;
+  }
+  int cnt = 0, dl = -1;
+  for (int j = -2; j <= 2; j++)
+    for (int i = -2; i <= 2; i++) {
+      int nl = (int)in[base + (long)(y + j) * W + (x + i)];
+      if (nl != cl) {
+        dl = nl;
+        cnt++;
+      }
+    }
+  out[idx] = (uint32_t)(cnt >= 16 ? dl : cl);
+}
+
+}  // namespace
+
+int launch_cvt(hipStream_t s, const uint8_t* rgbx, long npix, float* lab, uint8_t* l8) {
+  if (npix <= 0) return 0;
+  long blocks = (npix + 255) / 256;
+  if (blocks > 256L * 64) blocks = 256L * 64;
+  hipLaunchKernelGGL(k_cvt, dim3((unsigned)blocks), dim3(256), 0, s, (const uint32_t*)rgbx, npix, (float4*)lab, l8);
+  MVS_LAUNCH_CHECK("k_cvt");
+  return 0;
+}
+
+int launch_init_centers(hipStream_t s, const float* lab, int V, int W, int H, int S, float* spixl) {
+  int mw = map_dim(W, S), mh = map_dim(H, S);
+  hipLaunchKernelGGL(k_init_centers, dim3((mw + 63) / 64, mh, V), dim3(64), 0, s, (const float4*)lab, W, H, S, mw,
+                     mh, spixl);
+  MVS_LAUNCH_CHECK("k_init_centers");
+  return 0;
+}
+
+int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labels) {
+  int mw = map_dim(W, S);
+  hipLaunchKernelGGL(k_grid_labels, dim3((W + 255) / 256, H, V), dim3(256), 0, s, W, H, S, mw, labels);
+  MVS_LAUNCH_CHECK("k_grid_labels");
+  return 0;
+}
+
+int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
+                  float col_n, float weight, uint32_t* labels) {
+  int mw = map_dim(W, S), mh = map_dim(H, S);
+  hipLaunchKernelGGL(k_assign, dim3((W + 63) / 64, (H + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, spixl, W,
+                     H, S, mw, mh, xy_n, col_n, weight, labels);
+  MVS_LAUNCH_CHECK("k_assign");
+  return 0;
+}
+
+int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V, int W, int H, int S,
+                  float* spixl) {
+  int mw = map_dim(W, S), mh = map_dim(H, S);
+  int G = (int)__builtin_ceilf((float)(S * S * 9) / (float)(kLocal * kLocal));
+  int cpl = S * 3 / kLocal;
+  if (cpl <= 0) return arg_fail("SLIC update needs spixl_size >= 6 (cluster_per_line = 3S/16 > 0)");
+  size_t lds = sizeof(float) * 6 * (size_t)G;
+  if (lds > 64 * 1024) return arg_fail("spixl_size too large for the update kernel");
+  hipLaunchKernelGGL(k_update, dim3(mw * mh, V), dim3(256), lds, s, (const float4*)lab, labels, W, H, S, mw, mh, G,
+                     cpl, spixl);
+  MVS_LAUNCH_CHECK("k_update");
+  return 0;
+}
+
+int launch_suppress(hipStream_t s, const uint32_t* in, uint32_t* out, int V, int W, int H) {
+  hipLaunchKernelGGL(k_suppress, dim3((W + 255) / 256, H, V), dim3(256), 0, s, in, out, W, H);
+  MVS_LAUNCH_CHECK("k_suppress");
+  return 0;
+}
+
+}  // namespace mvs

@@ -1,0 +1,257 @@
+"""Device-side stage API on torch tensors, backed by libmvs.so (HIP, gfx950).
+
+torch supplies device memory, the HIP stream and ``torch.distributed``; every
+compute step is a hand-written HIP kernel reached through the C-ABI in
+include/mvs.h.  Tensors are in the reference layouts:
+
+    rgbx   uint8   [V, H, W, 4]     lab    float32 [V, H, W, 4]
+    spixl  float32 [V, mh, mw, 8]   labels int32   [V, H, W] (uint32 bits)
+    rep    uint8   [V, mh, mw, 8]   state  float32 [V, mh, mw, 6]
+    disp   float32 [V, H, W]
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .params import map_size
+
+
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("libmvs device API needs CUDA (HIP) tensors")
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return C.c_void_p(t.data_ptr())
+
+
+@dataclass
+class CameraArray:
+    """Host-side camera-array metadata (pipeline::perform_depth_est)."""
+    array_width: int
+    bl_ratio: float
+    levels: np.ndarray        # float32 [D]
+    view_subset: np.ndarray   # int32 [V, V]
+    subset_num: np.ndarray    # int32 [V]
+
+    def __post_init__(self):
+        self.levels = np.ascontiguousarray(self.levels, np.float32)
+        self.view_subset = np.ascontiguousarray(self.view_subset, np.int32)
+        self.subset_num = np.ascontiguousarray(self.subset_num, np.int32)
+        self._desc = _lib.ArrayDesc(
+            int(self.subset_num.shape[0]), int(self.array_width), float(self.bl_ratio),
+            self.levels.ctypes.data_as(C.POINTER(C.c_float)), int(self.levels.shape[0]),
+            self.view_subset.ctypes.data_as(C.POINTER(C.c_int32)),
+            self.subset_num.ctypes.data_as(C.POINTER(C.c_int32)))
+
+    @property
+    def view_count(self) -> int:
+        return int(self.subset_num.shape[0])
+
+    @property
+    def D(self) -> int:
+        return int(self.levels.shape[0])
+
+    def desc(self):
+        return C.byref(self._desc)
+
+
+class Engine:
+    """One libmvs context on one GPU (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self.L = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.MvsError("no GPU visible: the MI355X engine has no CPU fallback")
+        self.device = torch.device("cuda", device)
+        ctx = C.c_void_p()
+        _lib.check(self.L.mvs_create(device, C.byref(ctx)), "mvs_create")
+        self.ctx = ctx
+        self._levels_dev = {}
+
+    def close(self):
+        if self.ctx:
+            self.L.mvs_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        self.L.mvs_set_stream(self.ctx, C.c_void_p(s))
+
+    def empty(self, shape, dtype):
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    # ---- SLIC -------------------------------------------------------------
+    def cvt(self, rgbx: torch.Tensor, want_l8: bool = True):
+        V, H, W, _ = rgbx.shape
+        lab = self.empty((V, H, W, 4), torch.float32)
+        l8 = self.empty((V, H, W), torch.uint8) if want_l8 else None
+        self._stream()
+        _lib.check(self.L.mvs_cvt_d(self.ctx, _ptr(rgbx), V, W, H, _ptr(lab), _ptr(l8)), "mvs_cvt_d")
+        return lab, l8
+
+    def slic(self, lab: torch.Tensor, S: int, weight: float = 0.6, no_iter: int = 5, enforce_connectivity=False,
+             spixl=None, labels=None):
+        V, H, W, _ = lab.shape
+        mw, mh = map_size(W, H, S)
+        spixl = self.empty((V, mh, mw, 8), torch.float32) if spixl is None else spixl
+        labels = self.empty((V, H, W), torch.int32) if labels is None else labels
+        if spixl.shape != (V, mh, mw, 8) or labels.shape != (V, H, W):
+            raise ValueError("slic: output shapes do not match")
+        p = _lib.SlicParams(int(S), float(weight), int(no_iter), int(bool(enforce_connectivity)))
+        self._stream()
+        _lib.check(self.L.mvs_slic_d(self.ctx, _ptr(lab), V, W, H, C.byref(p), _ptr(spixl), _ptr(labels)),
+                   "mvs_slic_d")
+        return spixl, labels
+
+    def grid(self, lab: torch.Tensor, S: int):
+        V, H, W, _ = lab.shape
+        mw, mh = map_size(W, H, S)
+        spixl = torch.zeros((V, mh, mw, 8), dtype=torch.float32, device=self.device)
+        labels = self.empty((V, H, W), torch.int32)
+        self._stream()
+        _lib.check(self.L.mvs_grid_d(self.ctx, _ptr(lab), V, W, H, S, _ptr(spixl), _ptr(labels)), "mvs_grid_d")
+        return spixl, labels
+
+    # ---- photo-consistency ----------------------------------------------
+    def boundary(self, spixl: torch.Tensor, labels: torch.Tensor, S: int):
+        V, H, W = labels.shape
+        mw, mh = map_size(W, H, S)
+        rep = self.empty((V, mh, mw, 8), torch.uint8)
+        self._stream()
+        _lib.check(self.L.mvs_boundary_d(self.ctx, V, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep)),
+                   "mvs_boundary_d")
+        return rep
+
+    def sweep_spixl(self, lab, spixl, rep, cam: CameraArray, S: int, z0: int = 0, z1: int | None = None):
+        """initial_depth_estimation_v2 in place on spixl[..., 7]."""
+        V, H, W, _ = lab.shape
+        z1 = V if z1 is None else z1
+        self._stream()
+        _lib.check(self.L.mvs_sweep_spixl_d(self.ctx, W, H, S, _ptr(lab), _ptr(spixl), _ptr(rep), cam.desc(), z0, z1),
+                   "mvs_sweep_spixl_d")
+        return spixl
+
+    def sweep_pixel_sad(self, lab, cam: CameraArray, z0: int = 0, z1: int | None = None, out=None):
+        V, H, W, _ = lab.shape
+        z1 = V if z1 is None else z1
+        out = self.empty((z1 - z0, H, W), torch.float32) if out is None else out
+        self._stream()
+        _lib.check(self.L.mvs_sweep_pixel_sad_d(self.ctx, W, H, _ptr(lab), cam.desc(), z0, z1, _ptr(out)),
+                   "mvs_sweep_pixel_sad_d")
+        return out
+
+    def box_stats(self, l8, K: int = 5, out=None):
+        V, H, W = l8.shape
+        out = self.empty((V, H, W, 2), torch.int32) if out is None else out
+        self._stream()
+        _lib.check(self.L.mvs_box_stats_d(self.ctx, _ptr(l8), V, W, H, K, _ptr(out)), "mvs_box_stats_d")
+        return out
+
+    def ncc_volume(self, l8, box, cam: CameraArray, z: int, K: int = 5, out=None):
+        V, H, W = l8.shape
+        out = self.empty((cam.D, H, W), torch.float32) if out is None else out
+        self._stream()
+        _lib.check(self.L.mvs_ncc_volume_d(self.ctx, W, H, _ptr(l8), _ptr(box), cam.desc(), K, z, _ptr(out)),
+                   "mvs_ncc_volume_d")
+        return out
+
+    def levels_dev(self, cam: CameraArray) -> torch.Tensor:
+        key = cam.levels.tobytes()
+        t = self._levels_dev.get(key)
+        if t is None:
+            t = torch.from_numpy(cam.levels.copy()).to(self.device)
+            self._levels_dev[key] = t
+        return t
+
+    def wta(self, vol, levels: torch.Tensor, disp=None, conf=None, want_conf: bool = True):
+        D, H, W = vol.shape
+        disp = self.empty((H, W), torch.float32) if disp is None else disp
+        if want_conf and conf is None:
+            conf = self.empty((H, W), torch.float32)
+        self._stream()
+        _lib.check(self.L.mvs_wta_d(self.ctx, W, H, D, _ptr(vol), _ptr(levels), _ptr(disp),
+                                    _ptr(conf) if want_conf else None), "mvs_wta_d")
+        return disp, conf
+
+    # ---- refinement ------------------------------------------------------
+    def refine(self, spixl, labels, rep, cam: CameraArray, S: int, gamma=2.0, alpha=6.0, fuse=1.0, kernel_step=13,
+               kernel_size=1080, no_prop=5, fusion_compat=True, want_disp=True):
+        V, H, W = labels.shape
+        mw, mh = map_size(W, H, S)
+        flat = self.empty((V, mh, mw, 2), torch.float32)
+        st = self.empty((V, mh, mw, 6), torch.float32)
+        st2 = self.empty((V, mh, mw, 6), torch.float32)
+        disp = self.empty((V, H, W), torch.float32) if want_disp else None
+        p = _lib.RefineParams(float(gamma), float(alpha), float(fuse), int(kernel_step), int(kernel_size),
+                              int(no_prop), int(bool(fusion_compat)))
+        self._stream()
+        _lib.check(self.L.mvs_refine_d(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), cam.desc(),
+                                       C.byref(p), _ptr(flat), _ptr(st), _ptr(st2), _ptr(disp)), "mvs_refine_d")
+        final = st
+        if not fusion_compat and no_prop > 0:
+            final = st2 if (no_prop - 1) % 2 == 0 else st
+        return {"flat": flat, "state": final, "state_compat": st, "disp": disp}
+
+    def flatness(self, spixl, gamma: float):
+        V, mh, mw, _ = spixl.shape
+        flat = self.empty((V, mh, mw, 2), torch.float32)
+        self._stream()
+        _lib.check(self.L.mvs_flatness_d(self.ctx, V, mw, mh, _ptr(spixl), C.c_float(gamma), _ptr(flat)),
+                   "mvs_flatness_d")
+        return flat
+
+    def init_state(self, spixl, labels, rep, flat, cam: CameraArray, S, gamma, alpha, nks, kss, fuse):
+        V, H, W = labels.shape
+        mw, mh = map_size(W, H, S)
+        st = self.empty((V, mh, mw, 6), torch.float32)
+        self._stream()
+        _lib.check(self.L.mvs_init_state_d(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), _ptr(flat),
+                                           cam.desc(), C.c_float(gamma), C.c_float(alpha), int(nks), C.c_float(kss),
+                                           C.c_float(fuse), _ptr(st)), "mvs_init_state_d")
+        return st
+
+    def propagate(self, spixl, labels, rep, flat, cam: CameraArray, S, it, alpha, gamma, fuse, nks, kss, st_in,
+                  st_out, z0=0, z1=None):
+        V, H, W = labels.shape
+        z1 = V if z1 is None else z1
+        self._stream()
+        _lib.check(self.L.mvs_propagate_d(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), _ptr(flat),
+                                          cam.desc(), int(it), C.c_float(alpha), C.c_float(gamma), C.c_float(fuse),
+                                          int(nks), C.c_float(kss), _ptr(st_in), _ptr(st_out), int(z0), int(z1)),
+                   "mvs_propagate_d")
+        return st_out
+
+    def spixl_to_image(self, spixl, labels, state, S):
+        V, H, W = labels.shape
+        disp = self.empty((V, H, W), torch.float32)
+        self._stream()
+        _lib.check(self.L.mvs_spixl_to_image_d(self.ctx, V, W, H, S, _ptr(spixl), _ptr(labels), _ptr(state),
+                                               _ptr(disp)), "mvs_spixl_to_image_d")
+        return disp
+
+    def filter(self, disp_full, array_width: int, bl_ratio: float, fuse: float = 1.0, z0: int = 0, z1=None,
+               out=None):
+        V, H, W = disp_full.shape
+        z1 = V if z1 is None else z1
+        proj = self.empty((V, H, W), torch.float32)
+        out = torch.zeros((V, H, W), dtype=torch.float32, device=self.device) if out is None else out
+        self._stream()
+        _lib.check(self.L.mvs_filter_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio), C.c_float(fuse),
+                                       _ptr(disp_full), _ptr(proj), _ptr(out), int(z0), int(z1)), "mvs_filter_d")
+        return proj, out
+
+    def synchronize(self):
+        _lib.check(self.L.mvs_synchronize(self.ctx), "mvs_synchronize")

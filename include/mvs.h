@@ -1,0 +1,166 @@
+/* mvs.h -- C-ABI of the MI355X multi-view-stereo depth engine (libmvs.so).
+ *
+ * Drop-in boundary for the reference's hot path.  The reference has no plugin
+ * API: its host stage classes enqueue OpenCL kernels by name.  Each entry point
+ * below replaces one of those stage methods / kernel groups (file:line of the
+ * reference interface in the comment), takes the reference's data layouts
+ *  as plain pointers + sizes, and returns 0 or a negative
+ * MVS_E_* status (the reference prints cl_int errors and carries on;
+ * errorHandler, file_handler.cpp:97-113 -- here every failure is returned).
+ *
+ * Two flavours:
+ *   mvs_*      host pointers; copy in, run on the context's GPU, copy out,
+ *              synchronous (what the reference stage methods do).
+ *   mvs_*_d    device pointers, enqueued on the context's HIP stream, async.
+ *
+ * Layouts (all arrays view-major, row-major):
+ *   rgbx   uint8 [V][H][W][4]  s0=R, s1=G, s2=B (loadImageIn, file_handler.cpp:6-14)
+ *   lab    float [V][H][W][4]  CIE-Lab + pad  (cl_float3)
+ *   l8     uint8 [V][H][W]     8-bit intensity for the NCC cost (build-defined)
+ *   spixl  float [V][mh][mw][8] {id, cx, cy, L, a, b, count, disparity}
+ *   labels uint32 [V][H][W]    per-view superpixel index y*mw+x
+ *   rep    uint8 [V][mh][mw][8] ray extents {NW,W,SW,N,S,NE,E,SE}
+ *   levels float [D]           disparity hypotheses
+ *   view_subset int32 [V][V] (row z = neighbour list of z), subset_num int32 [V]
+ *   state  float [V][mh][mw][6] {d, sm, cs, nx, ny, nz}
+ *   disp   float [V][H][W]     disparity in pixels (depth-map output)
+ *   mw = ceil(W/S), mh = ceil(H/S) (pipeline.cpp:18-19)
+ *
+ * Not thread-safe per context.  One context per GPU; one process per GPU.
+ */
+#ifndef MVS_H
+#define MVS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  MVS_OK = 0,
+  MVS_E_ARG = -1,      /* invalid argument / shape */
+  MVS_E_HIP = -2,      /* HIP runtime error */
+  MVS_E_NOMEM = -3,    /* device allocation failed */
+  MVS_E_UNSUPPORTED = -4
+};
+
+typedef struct mvs_ctx mvs_ctx;
+
+/* SLIC parameters: system_settings fields used by clSLIC (header.h:55-77). */
+typedef struct {
+  int spixl_size;            /* S */
+  float color_weight;        /* slic_color_weight (clMVDE.cpp:16 = 0.6) */
+  int no_iter;               /* update/assign iterations (5) */
+  int enforce_connectivity;  /* supress_local_lable x2 (clSLIC.cpp:373-411) */
+} mvs_slic_params;
+
+/* Camera array / hypothesis set (pipeline::perform_depth_est).  Its arrays are
+ * small metadata and are HOST pointers in both API flavours; the context keeps
+ * a device copy (re-uploaded only when the contents change). */
+typedef struct {
+  int view_count;            /* V */
+  int array_width;           /* cameras per row */
+  float bl_ratio;            /* vertical / horizontal baseline ratio */
+  const float* levels;       /* [D] host pointer */
+  int num_levels;            /* D */
+  const int32_t* view_subset;/* [V][V] */
+  const int32_t* subset_num; /* [V] */
+} mvs_array;
+
+/* Refinement parameters (system_settings; clDepthRefinement::do_refinement). */
+typedef struct {
+  float gamma;               /* settings->gamma (2) */
+  float alpha;               /* settings->alpha (6) */
+  float fuse;                /* settings->fuse (1) */
+  int kernel_step;           /* settings->kernel_step (13) */
+  int kernel_size;           /* settings->kernel_size (1080) */
+  int no_prop;               /* propagate iterations (5) */
+  int fusion_compat;         /* 1: render current_state_dev as the reference does */
+} mvs_refine_params;
+
+/* ---- context ----------------------------------------------------------- */
+int mvs_create(int device, mvs_ctx** out);
+void mvs_destroy(mvs_ctx* ctx);
+const char* mvs_last_error(void);
+int mvs_set_stream(mvs_ctx* ctx, void* hip_stream);   /* NULL = default stream */
+int mvs_synchronize(mvs_ctx* ctx);
+const char* mvs_version(void);
+
+/* ---- device-pointer stage API ------------------------------------------ */
+/* cvt kernel (clcode.cl:125-151) over V views; l8 may be NULL. */
+int mvs_cvt_d(mvs_ctx* ctx, const uint8_t* rgbx, int V, int W, int H, float* lab, uint8_t* l8);
+
+/* SLIC on V views of lab (clSLIC::do_super_pixel_seg, clSLIC.cpp:67-122,
+ * minus the cvt it starts with).  spixl [V][mh][mw][8], labels [V][H][W]. */
+int mvs_slic_d(mvs_ctx* ctx, const float* lab, int V, int W, int H, const mvs_slic_params* p,
+               float* spixl, uint32_t* labels);
+
+/* SLIC-off grid mode: init_cluster_centers + init_label_per_pixl
+ * (clcode.cl:259-294, 341-353). */
+int mvs_grid_d(mvs_ctx* ctx, const float* lab, int V, int W, int H, int S, float* spixl, uint32_t* labels);
+
+/* find_super_pixel_boundary (clcode.cl:791-855; photo_consistency.cpp:88-110). */
+int mvs_boundary_d(mvs_ctx* ctx, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                   uint8_t* rep);
+
+/* initial_depth_estimation_v2 for reference views [z0, z1): writes spixl.s7
+ * (clcode.cl:972-1069; photo_consistency.cpp:113-140). */
+int mvs_sweep_spixl_d(mvs_ctx* ctx, int W, int H, int S, const float* lab, float* spixl, const uint8_t* rep,
+                      const mvs_array* a, int z0, int z1);
+
+/* The same sweep evaluated at S=1 grid semantics (per-pixel SAD, reference
+ * parity mode) without materialising spixl: disp [z1-z0][H][W]. */
+int mvs_sweep_pixel_sad_d(mvs_ctx* ctx, int W, int H, const float* lab, const mvs_array* a, int z0, int z1,
+                          float* disp);
+
+/* Build-defined per-pixel NCC KxK plane sweep.  box [V][H][W][2] int32 window
+ * sums of l8 (mvs_box_stats_d); vol [D][H][W] float cost of reference view z. */
+int mvs_box_stats_d(mvs_ctx* ctx, const uint8_t* l8, int V, int W, int H, int K, int32_t* box);
+int mvs_ncc_volume_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
+                     int K, int z, float* vol);
+/* Winner-take-all over vol [D][H][W]: disp = levels[first argmin], conf =
+ * (min cost outside best+-1) - best cost.  conf may be NULL. */
+int mvs_wta_d(mvs_ctx* ctx, int W, int H, int D, const float* vol, const float* levels, float* disp, float* conf);
+
+/* Superpixel-plane refinement (clDepthRefinement, depth_refinement.cpp:91-1470).
+ * flat [V][mh][mw][2] and state/state2 [V][mh][mw][6] are caller-provided
+ * workspaces; the final state is returned in *state (compat: see mvs_refine_params). */
+int mvs_flatness_d(mvs_ctx* ctx, int V, int mw, int mh, const float* spixl, float gamma, float* flat);
+int mvs_init_state_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                     const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
+                     int kernel_steps, float kss, float fuse, float* state);
+int mvs_propagate_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                    const uint8_t* rep, const float* flat, const mvs_array* a, int iter, float alpha,
+                    float gamma, float fuse, int kernel_steps, float kss, const float* st_in, float* st_out,
+                    int z0, int z1);
+int mvs_spixl_to_image_d(mvs_ctx* ctx, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                         const float* state, float* disp);
+int mvs_refine_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                 const uint8_t* rep, const mvs_array* a, const mvs_refine_params* p, float* flat,
+                 float* state, float* state2, float* disp);
+
+/* Cross-view consistency filter (clcode.cl:1995-2101, pinned order):
+ * project_to_reference_inv for all views, then remove_view_inconsistency for
+ * reference views [z0, z1).  proj/out [V][H][W]. */
+int mvs_filter_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, float fuse,
+                 const float* disp_full, float* proj, float* out, int z0, int z1);
+
+/* ---- host-pointer stage API (mirrors the reference stage methods) ------- */
+/* clSLIC::do_super_pixel_seg(in_img, lab_out, spixl_out, idx_out), one view. */
+int mvs_do_super_pixel_seg(mvs_ctx* ctx, const uint8_t* rgbx, int W, int H, const mvs_slic_params* p,
+                           float* lab, float* spixl, uint32_t* labels);
+/* clPhotoConsistency::do_initial_depth_estimation(spixl_inout, rep_out, lab,
+ * idx, array_width, bl_ratio, view_subset, disp_levels), all V views. */
+int mvs_do_initial_depth_estimation(mvs_ctx* ctx, int W, int H, int S, float* spixl, uint8_t* rep,
+                                    const float* lab, const uint32_t* labels, const mvs_array* a);
+/* clDepthRefinement(...)->do_refinement(...) + fusion output disp [V][H][W]. */
+int mvs_do_refinement(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                      const uint8_t* rep, const mvs_array* a, const mvs_refine_params* p, float* state_out,
+                      float* disp);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVS_H */

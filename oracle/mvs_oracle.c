@@ -1,0 +1,906 @@
+/* ORACLE TEST INFRASTRUCTURE -- CPU restatement of the reference hot path.
+ *
+ * PARITY UNPINNED: the reference (clMVDE/clcode.cl, OpenCL C) ships no tests,
+ * fixtures or golden vectors, and running its kernels (on the GPU box through
+ * the ROCm OpenCL runtime) was denied for this build; a CPU build would need a
+ * stand-in OpenCL runtime the image lacks.  This file restates the kernels'
+ * arithmetic from the reference source text, statement by statement, under the
+ * numerical definition in include/mvs_detmath.h (IEEE ops, no contraction,
+ * pinned builtins).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may call it, and only as the checker / CPU baseline.
+ *
+ * Layouts are the reference's: rgbx [H][W][4] u8 (s0=R),
+ * lab [H][W][4] f32, spixl [mh][mw][8] f32, labels [H][W] u32,
+ * rep [mh][mw][8] u8, levels [D] f32, view_subset [V][V] i32, subset_num [V].
+ * Multi-view arrays are view-major.
+ *
+ * Build: oracle/Makefile -> oracle/_build/liboracle.so (gcc -O3 -fopenmp
+ * -ffp-contract=off).  OpenMP only parallelises independent output elements.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mvs_detmath.h"
+
+#define LOCAL 16 /* LOCAL_SIZE_UPDATE, header.h:37-38 */
+
+static int imax(int a, int b) { return a > b ? a : b; }
+static int ceil_div_f(int a, int b) { return (int)ceilf((float)a / (float)b); }
+
+int orc_map_w(int W, int S) { return ceil_div_f(W, S); }
+int orc_map_h(int H, int S) { return ceil_div_f(H, S); }
+
+/* ------------------------------------------------------------------------ */
+/* rgb2lab + cvt, clcode.cl:21-59, 125-151.  s0 is read as BLUE (R/B swap). */
+/* ------------------------------------------------------------------------ */
+static void rgb2lab(uint8_t s0, uint8_t s1, uint8_t s2, float* out) {
+  float _b = (float)s0 * 0.0039216f;
+  float _g = (float)s1 * 0.0039216f;
+  float _r = (float)s2 * 0.0039216f;
+  float x = _r * 0.412453f + _g * 0.357580f + _b * 0.180423f;
+  float y = _r * 0.212671f + _g * 0.715160f + _b * 0.072169f;
+  float z = _r * 0.019334f + _g * 0.119193f + _b * 0.950227f;
+  const float epsilon = 0.008856f, kappa = 903.3f;
+  const float Xr = 0.950456f, Yr = 1.0f, Zr = 1.088754f;
+  float xr = x / Xr, yr = y / Yr, zr = z / Zr;
+  float fx, fy, fz;
+  const float third = 1.0f / 3.0f;
+  if (xr > epsilon) fx = mvs_powrf(xr, third); else fx = (kappa * xr + 16.0f) / 116.0f;
+  if (yr > epsilon) fy = mvs_powrf(yr, third); else fy = (kappa * yr + 16.0f) / 116.0f;
+  if (zr > epsilon) fz = mvs_powrf(zr, third); else fz = (kappa * zr + 16.0f) / 116.0f;
+  out[0] = 116.0f * fy - 16.0f;
+  out[1] = 500.0f * (fx - fy);
+  out[2] = 200.0f * (fy - fz);
+  out[3] = 0.0f;
+}
+
+void orc_cvt(const uint8_t* rgbx, int W, int H, float* lab) {
+  long n = (long)W * H;
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < n; i++) rgb2lab(rgbx[4 * i], rgbx[4 * i + 1], rgbx[4 * i + 2], lab + 4 * i);
+}
+
+/* Build-defined: 8-bit intensity plane for the NCC cost, q = clamp(int(L*2.55+0.5)). */
+void orc_l8(const float* lab, int W, int H, uint8_t* q) {
+  long n = (long)W * H;
+  for (long i = 0; i < n; i++) {
+    float t = lab[4 * i] * 2.55f;
+    t = t + 0.5f;
+    int v = (int)t;
+    q[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* init_cluster_centers, clcode.cl:259-294                                   */
+/* ------------------------------------------------------------------------ */
+void orc_init_centers(const float* lab, int W, int H, int S, float* spixl) {
+  int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+  for (int row = 0; row < mh; row++)
+    for (int col = 0; col < mw; col++) {
+      int ci = row * mw + col;
+      int cx = col * S + S / 2, cy = row * S + S / 2;
+      if (cx > W) cx = (col * S + W) / 2;
+      if (cy > H) cy = (row * S + H) / 2;
+      float* o = spixl + 8 * (long)ci;
+      o[0] = (float)ci;
+      o[1] = (float)cx;
+      o[2] = (float)cy;
+      long p = (long)cy * W + cx; /* may be W*H-or-beyond when cx == W: pinned to 0 */
+      if (p < (long)W * H) {
+        o[3] = lab[4 * p]; o[4] = lab[4 * p + 1]; o[5] = lab[4 * p + 2];
+      } else {
+        o[3] = o[4] = o[5] = 0.0f;
+      }
+      o[6] = 0.0f;
+    }
+}
+
+/* init_label_per_pixl, clcode.cl:341-353 */
+void orc_grid_labels(int W, int H, int S, uint32_t* labels) {
+  int mw = orc_map_w(W, S);
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) labels[(long)y * W + x] = (uint32_t)(mw * (y / S) + x / S);
+}
+
+/* ------------------------------------------------------------------------ */
+/* slic_distance_function + find_center_association, clcode.cl:422-520     */
+/* ------------------------------------------------------------------------ */
+static float slic_dist(const float* px, int y, int x, const float* c, float weight, float sn, float cn) {
+  float a = (px[0] - c[3]) * (px[0] - c[3]);
+  a = a + (px[1] - c[4]) * (px[1] - c[4]);
+  a = a + (px[2] - c[5]) * (px[2] - c[5]);
+  float b = ((float)x - c[1]) * ((float)x - c[1]);
+  b = b + ((float)y - c[2]) * ((float)y - c[2]);
+  float d = (a * cn) + weight * (b * sn);
+  return sqrtf(d);
+}
+
+void orc_assign(const float* lab, const float* spixl, int W, int H, int S, float xy_n, float col_n,
+                float weight, uint32_t* labels) {
+  int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+#pragma omp parallel for schedule(static)
+  for (int row = 0; row < H; row++)
+    for (int col = 0; col < W; col++) {
+      long pid = (long)row * W + col;
+      int cxg = col / S, cyg = row / S;
+      int dX = (col + S / 2) / S - cxg, dY = (row + S / 2) / S - cyg;
+      float min_dist = 999999.9999f, min_id = -1;
+      for (int i = -1 + dX; i <= dX; i++)       /* i spans the x delta ... */
+        for (int j = -1 + dY; j <= dY; j++) {   /* ... but offsets y (swapped) */
+          int cx = cxg + j, cy = cyg + i;
+          if (cx >= 0 && cy >= 0 && cx < mw && cy < mh) {
+            int ci = cy * mw + cx;
+            float d = slic_dist(lab + 4 * pid, row, col, spixl + 8 * (long)ci, weight, xy_n, col_n);
+            if (d < min_dist) { min_dist = d; min_id = (float)ci; }
+          }
+        }
+      labels[pid] = (uint32_t)min_id;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* update_cluster_center + finalize_reduction_result, clcode.cl:533-611,    */
+/* 719-773; launch shape clSLIC.cpp:307-370.  The 16x16 tile of each        */
+/* (superpixel, t) pair is reduced with the reference's LDS tree (stride    */
+/* 128..1, v[k] += v[k+i]); partials are summed in tile order.              */
+/* ------------------------------------------------------------------------ */
+void orc_update(const float* lab, const uint32_t* labels, int W, int H, int S, float* spixl) {
+  int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+  int G = (int)ceilf((float)(S * S * 9) / (float)(LOCAL * LOCAL));
+  int cpl = S * 3 / LOCAL;
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int sp = 0; sp < mw * mh; sp++) {
+    int gx = sp % mw, gy = sp / mw;
+    float acc[6] = {0, 0, 0, 0, 0, 0}; /* x, y, L, a, b, n  (finalize order) */
+    for (int t = 0; t < G; t++) {
+      float v[256][6];
+      memset(v, 0, sizeof(v));
+      int nbx = t % cpl, nby = t / cpl;
+      for (int ly = 0; ly < LOCAL; ly++)
+        for (int lx = 0; lx < LOCAL; lx++) {
+          int k = ly * LOCAL + lx;
+          int pxo = nbx * LOCAL + lx, pyo = nby * LOCAL + ly;
+          if (pyo < S * 3 && pxo < S * 3) {
+            int px = gx * S - S + pxo, py = gy * S - S + pyo;
+            if (py >= 0 && px >= 0 && px < W && py < H) {
+              long pi = (long)py * W + px;
+              if (labels[pi] == (uint32_t)sp) {
+                v[k][0] = (float)px; v[k][1] = (float)py;
+                v[k][2] = lab[4 * pi]; v[k][3] = lab[4 * pi + 1]; v[k][4] = lab[4 * pi + 2];
+                v[k][5] = 1.0f;
+              }
+            }
+          }
+        }
+      for (int i = 128; i != 0; i /= 2)
+        for (int k = 0; k < i; k++)
+          for (int c = 0; c < 6; c++) v[k][c] = v[k][c] + v[k + i][c];
+      for (int c = 0; c < 6; c++) acc[c] = acc[c] + v[0][c];
+    }
+    float* o = spixl + 8 * (long)sp;
+    o[0] = (float)sp;
+    o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
+    float n = acc[5];
+    if (n != 0) {
+      o[1] = acc[0] / n; o[2] = acc[1] / n;
+      o[3] = acc[2] / n; o[4] = acc[3] / n; o[5] = acc[4] / n;
+      o[6] = n;
+    }
+  }
+}
+
+/* supress_local_lable, clcode.cl:676-711 (one pass) */
+void orc_suppress(const uint32_t* in, uint32_t* out, int W, int H) {
+#pragma omp parallel for schedule(static)
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      long idx = (long)y * W + x;
+      int cl = (int)in[idx];
+      if (x <= 1 || y <= 1 || x >= W - 2 || y >= H - 2) { out[idx] = (uint32_t)cl; continue; }
+      int cnt = 0, dl = -1;
+      for (int j = -2; j <= 2; j++)
+        for (int i = -2; i <= 2; i++) {
+          int nl = (int)in[(long)(y + j) * W + (x + i)];
+          if (nl != cl) { dl = nl; cnt++; }
+        }
+      out[idx] = (uint32_t)(cnt >= 16 ? dl : cl);
+    }
+}
+
+/* clSLIC::do_super_pixel_seg, clSLIC.cpp:67-122 (edge path disabled) */
+void orc_slic(const uint8_t* rgbx, int W, int H, int S, float weight, int no_iter, int enforce_conn,
+              float* lab, float* spixl, uint32_t* labels) {
+  float xy = 1.0f / (1.4242f * (float)S);
+  float col = 15.0f / (1.7321f * 128.0f);
+  xy = xy * xy;
+  col = col * col;
+  orc_cvt(rgbx, W, H, lab);
+  orc_init_centers(lab, W, H, S, spixl);
+  orc_assign(lab, spixl, W, H, S, xy, col, weight, labels);
+  for (int i = 0; i < no_iter; i++) {
+    orc_update(lab, labels, W, H, S, spixl);
+    orc_assign(lab, spixl, W, H, S, xy, col, weight, labels);
+  }
+  if (enforce_conn) {
+    uint32_t* tmp = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)W * H);
+    orc_suppress(labels, tmp, W, H);
+    orc_suppress(tmp, labels, W, H);
+    free(tmp);
+  }
+}
+
+/* SLIC-off grid mode: cvt + init_cluster_centers + init_label_per_pixl */
+void orc_grid(const uint8_t* rgbx, int W, int H, int S, float* lab, float* spixl, uint32_t* labels) {
+  orc_cvt(rgbx, W, H, lab);
+  orc_init_centers(lab, W, H, S, spixl);
+  orc_grid_labels(W, H, S, labels);
+}
+
+/* ------------------------------------------------------------------------ */
+/* find_super_pixel_boundary, clcode.cl:791-855.  dir.k = (last i whose ray  */
+/* sample still carries the own label) - 1.                                  */
+/* ------------------------------------------------------------------------ */
+void orc_boundary(int V, int W, int H, int S, const float* spixl, const uint32_t* labels, uint8_t* rep) {
+  int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+  long M = (long)mw * mh, P = (long)W * H;
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int z = 0; z < V; z++)
+    for (long s = 0; s < M; s++) {
+      int tx = (int)(s % mw), ty = (int)(s / mw);
+      const float* sp = spixl + 8 * (z * M + s);
+      int cx = (int)sp[1], cy = (int)sp[2];
+      if (cx < S) cx += (S - cx);
+      if (cx + S > W) cx -= S;
+      if (cy < S) cy += (S - cy);
+      if (cy + S > H) cy -= S;
+      uint32_t id = (uint32_t)(ty * mw + tx);
+      const uint32_t* L = labels + z * P;
+      uint8_t dir[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define LBL(yy, xx) (((yy) >= 0 && (yy) < H && (xx) >= 0 && (xx) < W) ? L[(long)(yy) * W + (xx)] : 0xFFFFFFFFu)
+      for (int i = 1; i < S; i++) {
+        if (id == LBL(cy - i, cx - i) && cx - i >= 0 && cy - i >= 0) dir[0] = (uint8_t)(i - 1);
+        if (id == LBL(cy, cx - i) && cx - i >= 0) dir[1] = (uint8_t)(i - 1);
+        if (id == LBL(cy + i, cx - i) && cx - i >= 0 && cy + i < H) dir[2] = (uint8_t)(i - 1);
+        if (id == LBL(cy - i, cx) && cy - i >= 0) dir[3] = (uint8_t)(i - 1);
+        if (id == LBL(cy + i, cx) && cy + i < H) dir[4] = (uint8_t)(i - 1);
+        if (id == LBL(cy - i, cx + i) && cx + i < W && cy - i >= 0) dir[5] = (uint8_t)(i - 1);
+        if (id == LBL(cy, cx + i) && cx + i < W) dir[6] = (uint8_t)(i - 1);
+        if (id == LBL(cy + i, cx + i) && cx + i < W && cy + i < H) dir[7] = (uint8_t)(i - 1);
+      }
+#undef LBL
+      memcpy(rep + 8 * (z * M + s), dir, 8);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* initial_depth_estimation_v2, clcode.cl:972-1069; host loop               */
+/* photo_consistency.cpp:133-140 (one launch per reference view z).         */
+/* ------------------------------------------------------------------------ */
+void orc_sweep(int V, int W, int H, int S, const float* lab, float* spixl, const uint8_t* rep,
+               const float* levels, int D, const int* vs, const int* sn, int aw, float bl, int z0, int z1) {
+  int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+  long M = (long)mw * mh, P = (long)W * H;
+  for (int z = z0; z < z1; z++) {
+#pragma omp parallel for schedule(dynamic, 16)
+    for (long s = 0; s < M; s++) {
+      long idx = z * M + s;
+      const uint8_t* dr = rep + 8 * idx;
+      int bl_ = imax(dr[0], imax(dr[1], dr[2]));
+      int br_ = imax(dr[5], imax(dr[6], dr[7]));
+      int bt_ = imax(dr[0], imax(dr[3], dr[5]));
+      int bb_ = imax(dr[2], imax(dr[4], dr[7]));
+      float stx = (float)fmax(1.0, 0.25 * (double)(float)(bl_ + br_));
+      float sty = (float)fmax(1.0, 0.25 * (double)(float)(bt_ + bb_));
+      float cx = spixl[8 * idx + 1], cy = spixl[8 * idx + 2];
+      int rx = z % aw, ry = z / aw;
+      float cost = 1000000.0f, disp = 0.0f;
+      for (int dl = 0; dl < D; dl++) {
+        float d = levels[dl];
+        float mn = 1000000.0f;
+        for (int n = 0; n < sn[z]; n++) {
+          int view = vs[V * z + n];
+          int vx = view % aw, vy = view / aw;
+          float val = 0.0f;
+          for (int i = -2; i <= 2; i++)
+            for (int j = -2; j <= 2; j++) {
+              int xr = (int)(cx + (float)i * stx);
+              int yr = (int)(cy + (float)j * sty);
+              int xp = (int)((float)xr - d * (float)(vx - rx));
+              int yp = (int)((float)yr - (bl * d) * (float)(vy - ry));
+              val = val + 30.0f;
+              if (xr >= 0 && yr >= 0 && xp >= 0 && yp >= 0 && xr < W && yr < H && xp < W && yp < H) {
+                val = val - 30.0f;
+                const float* a = lab + 4 * (z * P + (long)yr * W + xr);
+                const float* b = lab + 4 * ((long)view * P + (long)yp * W + xp);
+                float ad = fabsf(a[0] - b[0]) + fabsf(a[1] - b[1]);
+                ad = ad + fabsf(a[2] - b[2]);
+                val = val + ad;
+              }
+            }
+          if (val < mn) mn = val;
+        }
+        if (mn < cost) { cost = mn; disp = d; }
+      }
+      spixl[8 * idx + 7] = disp;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Build-defined per-pixel NCC cost volume (no reference counterpart).      */
+/*   q = L8 intensity; window K x K (r = K/2); shift (tx, ty) =             */
+/*   (roundf(d*dx), roundf((bl*d)*dy)); window valid iff every tap of the   */
+/*   reference and the shifted window lies inside the image.                */
+/*   num = n*Srp - Sr*Sp, vr = n*Srr - Sr^2, vp = n*Spp - Sp^2 (int32).     */
+/*   cost = 2 (invalid) | 1 (vr==0 or vp==0) | 1 - a*|a| / (vr_f * vp_f)    */
+/*   with a = (float)num.  cost(d) = min over neighbours (strict <, init    */
+/*   1e6); vol[z][d][y][x].                                                  */
+/* ------------------------------------------------------------------------ */
+void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, int D, const int* vs,
+                    const int* sn, int aw, float bl, int K, int z, float* vol) {
+  int r = K / 2, nk = K * K;
+  long P = (long)W * H;
+  int rx = z % aw, ry = z / aw;
+  const uint8_t* qr = q + z * P;
+#pragma omp parallel for schedule(static)
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      int rin = (x - r >= 0 && x + r < W && y - r >= 0 && y + r < H);
+      int Sr = 0, Srr = 0;
+      if (rin)
+        for (int j = -r; j <= r; j++)
+          for (int i = -r; i <= r; i++) {
+            int a = qr[(long)(y + j) * W + x + i];
+            Sr += a; Srr += a * a;
+          }
+      int vr = nk * Srr - Sr * Sr;
+      for (int dl = 0; dl < D; dl++) {
+        float d = levels[dl];
+        float mn = 1000000.0f;
+        for (int n = 0; n < sn[z]; n++) {
+          int view = vs[V * z + n];
+          int dx = view % aw - rx, dy = view / aw - ry;
+          int tx = (int)roundf(d * (float)dx);
+          int ty = (int)roundf((bl * d) * (float)dy);
+          int px = x - tx, py = y - ty;
+          float c;
+          if (!rin || px - r < 0 || px + r >= W || py - r < 0 || py + r >= H) {
+            c = 2.0f;
+          } else {
+            const uint8_t* qp = q + (long)view * P;
+            int Sp = 0, Spp = 0, Srp = 0;
+            for (int j = -r; j <= r; j++)
+              for (int i = -r; i <= r; i++) {
+                int a = qr[(long)(y + j) * W + x + i];
+                int b = qp[(long)(py + j) * W + px + i];
+                Sp += b; Spp += b * b; Srp += a * b;
+              }
+            int vp = nk * Spp - Sp * Sp;
+            int num = nk * Srp - Sr * Sp;
+            if (vr == 0 || vp == 0) {
+              c = 1.0f;
+            } else {
+              float a = (float)num;
+              float bb = a * fabsf(a);
+              float cc = (float)vr * (float)vp;
+              c = 1.0f - bb / cc;
+            }
+          }
+          if (c < mn) mn = c;
+        }
+        vol[((long)dl * H + y) * W + x] = mn;
+      }
+    }
+}
+
+/* Build-defined WTA over a cost volume [D][H][W]: first minimum (strict <,
+ * init 1e6, disparity levels[0]-less default 0), confidence = c2 - c1 where
+ * c2 = min cost over levels outside {best-1, best, best+1} (0 if none). */
+void orc_wta(int W, int H, int D, const float* vol, const float* levels, float* disp, float* conf) {
+  long P = (long)W * H;
+#pragma omp parallel for schedule(static)
+  for (long p = 0; p < P; p++) {
+    float best = 1000000.0f, dsp = 0.0f;
+    int bi = -1;
+    for (int dl = 0; dl < D; dl++) {
+      float c = vol[dl * P + p];
+      if (c < best) { best = c; dsp = levels[dl]; bi = dl; }
+    }
+    float c2 = 1000000.0f;
+    for (int dl = 0; dl < D; dl++) {
+      if (dl >= bi - 1 && dl <= bi + 1) continue;
+      float c = vol[dl * P + p];
+      if (c < c2) c2 = c;
+    }
+    disp[p] = dsp;
+    if (conf) conf[p] = (bi < 0 || c2 == 1000000.0f) ? 0.0f : c2 - best;
+  }
+}
+
+/* ======================================================================== */
+/* Superpixel-plane refinement, clcode.cl:1076-1931; host schedule          */
+/* clDepthRefinement::do_refinement, depth_refinement.cpp:91-118.           */
+/* state layout [V][mh][mw][6] = {d, sm, cs, nx, ny, nz}.                   */
+/* ======================================================================== */
+typedef struct {
+  int V, W, H, S, mw, mh, aw;
+  long M, P;
+  const float* spixl;
+  const uint32_t* labels;
+  const uint8_t* rep;
+  const float* flat;
+  const int* vs;
+  const int* sn;
+  float bl, fuse, alpha, gamma;
+} rctx;
+
+static float expf_neg_sq(float diff, float k) { return mvs_expf(((-diff) * diff) * k); }
+
+/* compute_flatness, clcode.cl:1076-1132 */
+void orc_flatness(int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
+  long M = (long)mw * mh;
+  for (int z = 0; z < V; z++)
+    for (int y = 0; y < mh; y++)
+      for (int x = 0; x < mw; x++) {
+        long idx = M * z + (long)mw * y + x;
+        const float* c0 = spixl + 8 * idx + 3;
+        float fl = 1.0f;
+        long nb[4];
+        int ok[4] = {x - 1 >= 0, x + 1 < mw, y + 1 < mh, y - 1 >= 0};
+        nb[0] = idx - 1; nb[1] = idx + 1; nb[2] = idx + mw; nb[3] = idx - mw;
+        for (int k = 0; k < 4; k++) {
+          if (!ok[k]) continue;
+          const float* c1 = spixl + 8 * nb[k] + 3;
+          float diff = (c1[0] - c0[0]) * (c1[0] - c0[0]);
+          diff = diff + (c1[1] - c0[1]) * (c1[1] - c0[1]);
+          diff = diff + (c1[2] - c0[2]) * (c1[2] - c0[2]);
+          fl = fl + diff;
+        }
+        flat[2 * idx] = mvs_expf((-fl) * gamma);
+        flat[2 * idx + 1] = (float)(1.0 - mvs_exp((-0.25 * (double)fl) * (double)gamma));
+      }
+}
+
+static int step_size_of(float flx, float kss) {
+  int s = (int)((double)(flx * kss) + 0.5);
+  return s > 1 ? s : 1;
+}
+
+/* init_smoothness, clcode.cl:1136-1254 */
+static float init_smoothness(const rctx* c, const float* sp_ref, const float* fl, int x, int y, int z,
+                             int nks, float kss) {
+  float sm = 0.0f, wn = 0.0f;
+  float cl0 = sp_ref[3], cl1 = sp_ref[4], cl2 = sp_ref[5], disp = sp_ref[7];
+  for (int i = -1; i <= 1; i++)
+    for (int j = -1; j <= 1; j++) {
+      int px = x + i, py = y + j;
+      if (px >= 0 && py >= 0 && px < c->mw && py < c->mh && (i != 0 || j != 0)) {
+        const float* s = c->spixl + 8 * (c->M * z + (long)c->mw * py + px);
+        float diff = mvs_distance3(s[3], s[4], s[5], cl0, cl1, cl2);
+        float simi = expf_neg_sq(diff, c->gamma);
+        diff = disp - s[7];
+        sm = sm + simi * expf_neg_sq(diff, c->alpha);
+        wn = wn + simi;
+      }
+    }
+  int ss = step_size_of(fl[0], kss);
+  for (int i = 1; i <= nks; i++) {
+    float gi = c->gamma * (float)(1 + i);
+    int step = i * ss;
+    int cand[4][2] = {{x - (step + 1), y}, {x + (step + 1), y}, {x, y - step - 1}, {x, y + step + 1}};
+    int ok[4] = {x > step, x < c->mw - step - 1, y > step, y < c->mh - step - 1};
+    for (int k = 0; k < 4; k++) {
+      if (!ok[k]) continue;
+      const float* s = c->spixl + 8 * (c->M * z + (long)c->mw * cand[k][1] + cand[k][0]);
+      float diff = mvs_distance3(cl0, cl1, cl2, s[3], s[4], s[5]);
+      float simi = expf_neg_sq(diff, gi);
+      diff = disp - s[7];
+      sm = sm + simi * expf_neg_sq(diff, c->alpha);
+      wn = wn + simi;
+    }
+  }
+  return wn > 0 ? sm / wn : 0.000001f;
+}
+
+static void samples_of(const uint8_t* r, int* s) {
+  s[0] = r[0]; s[1] = r[1]; s[2] = r[2]; s[3] = r[3]; s[4] = 0;
+  s[5] = r[4]; s[6] = r[5]; s[7] = r[6]; s[8] = r[7];
+}
+
+static float finish_consistency(float cons, int vc) {
+  float margin = 0.01f;
+  if (vc > 0) return fmaxf(margin, cons / (float)vc);
+  return margin;
+}
+
+/* initialize_consistency, clcode.cl:1260-1357 */
+static float init_consistency(const rctx* c, int x, int y, int z, const float* color, const float* center,
+                              float d, const float* fl) {
+  float cons = 0.0f;
+  int vc = 0;
+  int camx = z % c->aw, camy = z / c->aw;
+  int smp[9];
+  samples_of(c->rep + 8 * (c->M * z + (long)c->mw * y + x), smp);
+  for (int n = 0; n < c->sn[z]; n++) {
+    int view = c->vs[z * c->V + n];
+    int vx = view % c->aw, vy = view / c->aw;
+    float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
+    for (int i = -1; i <= 1; i++)
+      for (int j = -1; j <= 1; j++) {
+        int xr = (int)center[0] + smp[(i + 1) * 3 + j + 1] * i;
+        int yr = (int)center[1] + smp[(i + 1) * 3 + j + 1] * j;
+        int xp = (int)((float)xr - roundf(d * (float)(vx - camx)));
+        int yp = (int)((float)yr - roundf((c->bl * d) * (float)(vy - camy)));
+        if (xp >= 0 && yp >= 0 && xp < c->W && yp < c->H) {
+          uint32_t ip = c->labels[c->P * view + (long)c->W * yp + xp];
+          uint32_t cx = ip % (uint32_t)c->mw, cy = ip / (uint32_t)c->mw;
+          const float* s = c->spixl + 8 * (c->M * view + (long)c->mw * cy + cx);
+          float diff = s[7] - d;
+          float wv = 0.0f;
+          if (fabsf(diff) < c->fuse) wv = 1.0f;
+          visible = visible + wv * expf_neg_sq(diff, c->alpha);
+          vis_w = vis_w + wv;
+          occ_w = occ_w + (1.0f - wv);
+          diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+          visibility = visibility + expf_neg_sq(diff, c->gamma);
+          num = num + 1.0f;
+        }
+      }
+    if (num > 0) {
+      vc++;
+      if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+      if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)fl[1]);
+    }
+  }
+  return finish_consistency(cons, vc);
+}
+
+/* init_current_state, clcode.cl:1362-1404 */
+void orc_init_state(int V, int W, int H, int S, int aw, float bl, const float* spixl, const uint32_t* labels,
+                    const uint8_t* rep, const float* flat, const int* vs, const int* sn, float gamma,
+                    float alpha, int nks, float kss, float fuse, float* state) {
+  rctx c = {V, W, H, S, orc_map_w(W, S), orc_map_h(H, S), aw, 0, (long)W * H, spixl, labels, rep, flat,
+            vs, sn, bl, fuse, alpha, gamma};
+  c.M = (long)c.mw * c.mh;
+#pragma omp parallel for collapse(2) schedule(dynamic, 8)
+  for (int z = 0; z < V; z++)
+    for (long s = 0; s < c.M; s++) {
+      int x = (int)(s % c.mw), y = (int)(s / c.mw);
+      long idx = c.M * z + s;
+      const float* sp = spixl + 8 * idx;
+      const float* fl = flat + 2 * idx;
+      float sm = init_smoothness(&c, sp, fl, x, y, z, nks, kss);
+      float cs = init_consistency(&c, x, y, z, sp + 3, sp + 1, sp[7], fl);
+      float* o = state + 6 * idx;
+      o[0] = sp[7]; o[1] = sm; o[2] = cs; o[3] = 0.0f; o[4] = 0.0f; o[5] = 1.0f;
+    }
+}
+
+static float plane_at(const float* n, float cx, float cy, float d, float px, float py) {
+  float t = n[0] * (cx - px);
+  t = t + n[1] * (cy - py);
+  t = t + n[2] * d;
+  return t / n[2];
+}
+
+/* compute_smoothness, clcode.cl:1407-1525 */
+static float comp_smoothness(const rctx* c, const float* st, float d, const float* nv, const float* center,
+                             const float* color, int x, int y, int z, const float* fl, int nks, float kss) {
+  float sm = 0.0f, wn = 0.0f;
+  for (int i = -1; i <= 1; i++)
+    for (int j = -1; j <= 1; j++) {
+      int px = x + i, py = y + j;
+      if (px >= 0 && py >= 0 && px < c->mw && py < c->mh && (i != 0 || j != 0)) {
+        long q = c->M * z + (long)c->mw * py + px;
+        const float* s = c->spixl + 8 * q;
+        float diff = mvs_distance3(color[0], color[1], color[2], s[3], s[4], s[5]);
+        float simi = expf_neg_sq(diff, c->gamma);
+        float di = plane_at(nv, center[0], center[1], d, s[1], s[2]);
+        diff = di - st[6 * q];
+        sm = sm + simi * expf_neg_sq(diff, c->alpha);
+        wn = wn + simi;
+      }
+    }
+  int ss = step_size_of(fl[0], kss);
+  for (int i = 1; i <= nks; i++) {
+    float gi = c->gamma * (float)(1 + i);
+    int step = i * ss;
+    int cand[4][2] = {{x - (step + 1), y}, {x + (step + 1), y}, {x, y - (step + 1)}, {x, y + (step + 1)}};
+    int ok[4] = {x > step, x < c->mw - step - 1, y > step, y < c->mh - step - 1};
+    for (int k = 0; k < 4; k++) {
+      if (!ok[k]) continue;
+      long q = c->M * z + (long)c->mw * cand[k][1] + cand[k][0];
+      const float* s = c->spixl + 8 * q;
+      float diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+      float simi = expf_neg_sq(diff, gi);
+      float de = plane_at(nv, center[0], center[1], d, s[1], s[2]);
+      diff = de - st[6 * q];
+      sm = sm + simi * expf_neg_sq(diff, c->alpha);
+      wn = wn + simi;
+    }
+  }
+  return wn > 0 ? sm / wn : 0.000001f;
+}
+
+/* compute_consistency, clcode.cl:1528-1631 (view_subset stride = V) */
+static float comp_consistency(const rctx* c, const float* st, const uint8_t* rep, float d, const float* nv,
+                              const float* center, const float* color, int x, int y, int z, const float* fl) {
+  (void)x; (void)y;
+  float cons = 0.0f;
+  int vc = 0;
+  int camx = z % c->aw, camy = z / c->aw;
+  int smp[9];
+  samples_of(rep, smp);
+  for (int k = 0; k < c->sn[z]; k++) {
+    int view = c->vs[c->V * z + k];
+    float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
+    int vx = view % c->aw, vy = view / c->aw;
+    for (int i = -1; i <= 1; i++)
+      for (int j = -1; j <= 1; j++) {
+        int sx = (int)center[0] + smp[(i + 1) * 3 + j + 1] * i;
+        int sy = (int)center[1] + smp[(i + 1) * 3 + j + 1] * j;
+        float di = plane_at(nv, center[0], center[1], d, (float)sx, (float)sy);
+        int xp = (int)((float)sx - roundf(di * (float)(vx - camx)));
+        int yp = (int)((float)sy - roundf((c->bl * di) * (float)(vy - camy)));
+        if (xp >= 0 && yp >= 0 && xp < c->W && yp < c->H) {
+          uint32_t ip = c->labels[c->P * view + (long)c->W * yp + xp];
+          uint32_t cx = ip % (uint32_t)c->mw, cy = ip / (uint32_t)c->mw;
+          long q = c->M * view + (long)c->mw * cy + cx;
+          const float* s = c->spixl + 8 * q;
+          const float* sq = st + 6 * q;
+          float dip = plane_at(sq + 3, s[1], s[2], sq[0], (float)xp, (float)yp);
+          float diff = dip - di;
+          float wv = 0.0f;
+          if (fabsf(diff) < c->fuse) wv = 1.0f;
+          visible = visible + wv * expf_neg_sq(diff, c->alpha);
+          vis_w = vis_w + wv;
+          occ_w = occ_w + (1.0f - wv);
+          diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+          visibility = visibility + expf_neg_sq(diff, c->gamma);
+          num = num + 1.0f;
+        }
+      }
+    if (num > 0) {
+      vc++;
+      if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+      if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)fl[1]);
+    }
+  }
+  return finish_consistency(cons, vc);
+}
+
+typedef struct { float d, sm, cs, n[3]; } pstate;
+
+/* update, clcode.cl:1635-1673 */
+static void plane_update(const rctx* c, const float* st, const uint8_t* rep, int iter, int nks, float kss,
+                         int x, int y, int z, const float* color, const float* center, const float* fl,
+                         long q, pstate* cur) {
+  const float* s1 = st + 6 * q;
+  float n1[3] = {s1[3], s1[4], s1[5]};
+  float d1 = s1[0];
+  const float* sc = c->spixl + 8 * q;
+  float t = n1[0] * (sc[1] - center[0]);
+  t = t + n1[1] * (sc[2] - center[1]);
+  t = t + n1[2] * d1;
+  float di = t / n1[2];
+  float sm1 = comp_smoothness(c, st, di, n1, center, color, x, y, z, fl, nks, kss);
+  float cs1 = comp_consistency(c, st, rep, di, n1, center, color, x, y, z, fl);
+  float diff = mvs_distance3(color[0], color[1], color[2], sc[3], sc[4], sc[5]);
+  float simi = expf_neg_sq(diff, c->gamma);
+  if ((iter < 4 && sm1 * simi > cur->sm) || cs1 * sm1 > cur->sm * cur->cs) {
+    cur->d = di; cur->sm = sm1; cur->cs = cs1;
+    cur->n[0] = n1[0]; cur->n[1] = n1[1]; cur->n[2] = n1[2];
+  }
+}
+
+static void normalize4(float* v) {
+  float s = v[0] * v[0];
+  s = s + v[1] * v[1];
+  s = s + v[2] * v[2];
+  s = s + v[3] * v[3];
+  if (s == 0.0f) return;
+  float r = sqrtf(s);
+  v[0] = v[0] / r; v[1] = v[1] / r; v[2] = v[2] / r; v[3] = v[3] / r;
+}
+
+/* spatialRefinement + cross_product_test, clcode.cl:1676-1723 */
+static void spatial_refine(const rctx* c, const float* st, const uint8_t* rep, int iter, int nks, float kss,
+                           int x, int y, int z, const float* color, const float* center, const float* fl,
+                           int n1x, int n1y, int n2x, int n2y, pstate* cur) {
+  long q1 = c->M * z + (long)c->mw * n1y + n1x, q2 = c->M * z + (long)c->mw * n2y + n2x;
+  const float* a1 = c->spixl + 8 * q1;
+  const float* a2 = c->spixl + 8 * q2;
+  float v1[3] = {a1[1] - center[0], a1[2] - center[1], st[6 * q1] - cur->d};
+  float v2[3] = {a2[1] - center[0], a2[2] - center[1], st[6 * q2] - cur->d};
+  float n[4];
+  n[0] = v1[1] * v2[2] - v1[2] * v2[1];
+  n[1] = v2[0] * v1[2] - v1[0] * v2[2];
+  n[2] = v1[0] * v2[1] - v1[1] * v2[0];
+  n[3] = 0.0f;
+  normalize4(n);
+  float sm1 = comp_smoothness(c, st, cur->d, n, center, color, x, y, z, fl, nks, kss);
+  float cs1 = comp_consistency(c, st, rep, cur->d, n, center, color, x, y, z, fl);
+  if ((iter < 4 && sm1 > cur->sm) || sm1 * cs1 > cur->sm * cur->cs) {
+    cur->sm = sm1; cur->cs = cs1;
+    cur->n[0] = n[0]; cur->n[1] = n[1]; cur->n[2] = n[2];
+  }
+}
+
+/* propagate, clcode.cl:1727-1900: one Jacobi iteration, in -> out.
+ * nks / kss are the per-iteration values (depth_refinement.cpp:768-769). */
+void orc_propagate(int V, int W, int H, int S, int aw, float bl, const float* spixl, const uint32_t* labels,
+                   const uint8_t* rep, const float* flat, const int* vs, const int* sn, int iter, float alpha,
+                   float gamma, float fuse, int nks, float kss, const float* st_in, float* st_out, int z0, int z1) {
+  rctx c = {V, W, H, S, orc_map_w(W, S), orc_map_h(H, S), aw, 0, (long)W * H, spixl, labels, rep, flat,
+            vs, sn, bl, fuse, alpha, gamma};
+  c.M = (long)c.mw * c.mh;
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
+  for (int z = z0; z < z1; z++)
+    for (long s = 0; s < c.M; s++) {
+      int x = (int)(s % c.mw), y = (int)(s / c.mw);
+      long idx = c.M * z + s;
+      const float* sp = spixl + 8 * idx;
+      float center[2] = {sp[1], sp[2]};
+      float color[3] = {sp[3], sp[4], sp[5]};
+      const float* si = st_in + 6 * idx;
+      pstate cur = {si[0], si[1], si[2], {si[3], si[4], si[5]}};
+      const float* fl = flat + 2 * idx;
+      const uint8_t* rp = rep + 8 * idx;
+      for (int i = -1; i <= 1; i++)
+        for (int j = -1; j <= 1; j++) {
+          int px = x + i, py = y + j;
+          if (px >= 0 && py >= 0 && px < c.mw && py < c.mh && !(i == 0 && j == 0))
+            plane_update(&c, st_in, rp, iter, nks, kss, x, y, z, color, center, fl, c.M * z + (long)c.mw * py + px, &cur);
+        }
+      int ssz = (int)kss;
+      for (int i = 1; i <= nks; i++) {
+        int off = i * ssz;
+        if (y > off) plane_update(&c, st_in, rp, iter, nks, kss, x, y, z, color, center, fl, c.M * z + (long)c.mw * (y - (off + 1)) + x, &cur);
+        if (y < c.mh - off - 1) plane_update(&c, st_in, rp, iter, nks, kss, x, y, z, color, center, fl, c.M * z + (long)c.mw * (y + off + 1) + x, &cur);
+        if (x > off) plane_update(&c, st_in, rp, iter, nks, kss, x, y, z, color, center, fl, c.M * z + (long)c.mw * y + (x - off - 1), &cur);
+        if (x < c.mw - off - 1) plane_update(&c, st_in, rp, iter, nks, kss, x, y, z, color, center, fl, c.M * z + (long)c.mw * y + (x + off + 1), &cur);
+      }
+      int nb[8][2] = {{x - 1, y}, {x - 1, y - 1}, {x, y - 1}, {x + 1, y - 1}, {x + 1, y}, {x + 1, y + 1}, {x, y + 1}, {x - 1, y + 1}};
+      for (int i = 0; i < 8; i++) {
+        int j = (i + 1) % 8;
+        if (nb[i][0] > -1 && nb[i][1] > -1 && nb[i][0] < c.mw && nb[i][1] < c.mh && nb[j][0] > -1 &&
+            nb[j][1] > -1 && nb[j][0] < c.mw && nb[j][1] < c.mh)
+          spatial_refine(&c, st_in, rp, iter, nks, kss, x, y, z, color, center, fl, nb[i][0], nb[i][1], nb[j][0], nb[j][1], &cur);
+      }
+      float* o = st_out + 6 * idx;
+      o[0] = cur.d; o[1] = cur.sm; o[2] = cur.cs; o[3] = cur.n[0]; o[4] = cur.n[1]; o[5] = cur.n[2];
+    }
+}
+
+/* spixl_to_image, clcode.cl:1906-1931 */
+void orc_spixl_to_image(int V, int W, int H, int S, const float* spixl, const uint32_t* labels, const float* st,
+                        float* disp) {
+  int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+  long M = (long)mw * mh, P = (long)W * H;
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int z = 0; z < V; z++)
+    for (int y = 0; y < H; y++)
+      for (int x = 0; x < W; x++) {
+        int id = (int)labels[P * z + (long)W * y + x];
+        int sx = id % mw, sy = id / mw;
+        long q = M * z + (long)mw * sy + sx;
+        const float* s = spixl + 8 * q;
+        const float* t = st + 6 * q;
+        float v = t[3] * (s[1] - (float)x);
+        v = v + t[4] * (s[2] - (float)y);
+        v = v + t[5] * t[0];
+        disp[P * z + (long)W * y + x] = v / t[5];
+      }
+}
+
+/* project_to_reference_inv + remove_view_inconsistency, clcode.cl:1995-2101,
+ * pinned order: every projection slice first, then every stability vote. */
+void orc_filter(int V, int W, int H, int aw, float bl, float fuse, const float* full, float* proj, float* view_out) {
+  long P = (long)W * H;
+  for (int r = 0; r < V; r++) {
+    int crx = r % aw, cry = r / aw;
+#pragma omp parallel for schedule(static)
+    for (long p = 0; p < P; p++) {
+      int x = (int)(p % W), y = (int)(p / W);
+      float md = full[P * r + p];
+      for (int i = 0; i < V; i++) {
+        if (i == r) continue;
+        int cx = i % aw, cy = i / aw;
+        int xp = (int)((float)x - roundf(md * (float)(crx - cx)));
+        int yp = (int)((float)y - roundf((bl * md) * (float)(cry - cy)));
+        if (xp >= 0 && yp >= 0 && xp < W && yp < H) {
+          float cd = full[P * i + (long)W * yp + xp];
+          if (md < cd) md = cd;
+        }
+      }
+      proj[P * r + p] = md;
+    }
+  }
+  for (int r = 0; r < V; r++) {
+    int crx = r % aw, cry = r / aw;
+#pragma omp parallel for schedule(static)
+    for (long p = 0; p < P; p++) {
+      int x = (int)(p % W), y = (int)(p / W);
+      float dest = 0.0f;
+      for (int i = 0; i < V; i++) {
+        float d = proj[P * i + p];
+        if (d != 0) {
+          float stab = 0.0f;
+          for (int j = 0; j < V; j++) {
+            float dc = proj[P * j + p];
+            if (dc != 0) {
+              float diff = dc - d;
+              if (fabsf(diff) > fuse) stab = stab - 1.0f;
+              if (fabsf(diff) <= fuse) stab = stab + 1.0f;
+            }
+          }
+          for (int j = 0; j < V; j++) {
+            int cx = j % aw, cy = j / aw;
+            int xx = (int)((float)x - roundf(d * (float)(cx - crx)));
+            int yy = (int)((float)y - roundf((bl * d) * (float)(cy - cry)));
+            if (xx >= 0 && yy >= 0 && xx < W && yy < H) {
+              float dc = full[P * j + (long)W * yy + xx];
+              float diff = dc - d;
+              if (fabsf(diff) > fuse) stab = stab - 1.0f;
+              if (fabsf(diff) < fuse) stab = stab + 1.0f;
+            }
+          }
+          if (stab >= 0 && (dest == 0 || dest < d)) dest = d;
+        }
+      }
+      view_out[P * r + p] = dest;
+    }
+  }
+}
+
+/* clDepthRefinement::do_refinement (flatness -> init -> no_prop x propagate
+ * ping-pong -> fusion).  Scalars are the host derivations of
+ * depth_refinement.cpp / pipeline.cpp:164-166 for gamma_s, alpha_s, fuse_s.
+ * fusion_compat: render current_state_dev as the reference does (last odd
+ * iteration); else the final iteration.  states (nullable) receives every
+ * iteration's output [no_prop][V][mh][mw][6]. */
+void orc_refine(int V, int W, int H, int S, int aw, float bl, const float* spixl, const uint32_t* labels,
+                const uint8_t* rep, const int* vs, const int* sn, float gamma_s, float alpha_s, float fuse_s,
+                int kernel_step, int kernel_size_full, int no_prop, int fusion_compat, float* flat, float* state0,
+                float* states, float* disp) {
+  int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+  long M = (long)mw * mh;
+  float gamma_ = (float)(2.0 * pow((double)gamma_s, 2.0));
+  float alpha_ = (float)(2.0 * pow((double)alpha_s, 2.0));
+  int kernel_size = kernel_size_full / 2;
+  int nks = kernel_step;
+  int kss_i = kernel_size / nks * S;
+  float kss = (float)(kss_i > 1 ? kss_i : 1);
+  float fuse = (float)(0.5 * (double)fuse_s);
+  orc_flatness(V, mw, mh, spixl, (float)(1.0 / (double)(float)gamma_), flat);
+  float* st = (float*)malloc(sizeof(float) * 6 * V * M);
+  float* st2 = (float*)malloc(sizeof(float) * 6 * V * M);
+  orc_init_state(V, W, H, S, aw, bl, spixl, labels, rep, flat, vs, sn, 1.0f / gamma_, 1.0f / alpha_, nks, kss,
+                 fuse, st);
+  if (state0) memcpy(state0, st, sizeof(float) * 6 * V * M);
+  memcpy(st2, st, sizeof(float) * 6 * V * M);
+  float pg = (float)(1.0 / (double)gamma_), pa = (float)(1.0 / (double)alpha_);
+  for (int it = 0; it < no_prop; it++) {
+    float* out = (it % 2 == 0) ? st2 : st;
+    float* in = (it % 2 == 0) ? st : st2;
+    orc_propagate(V, W, H, S, aw, bl, spixl, labels, rep, flat, vs, sn, it, pa, pg, fuse, nks / (it + 1),
+                  kss / (float)(it + 1), in, out, 0, V);
+    if (states) memcpy(states + (long)it * 6 * V * M, out, sizeof(float) * 6 * V * M);
+  }
+  if (disp) {
+    float* src = st;
+    if (!fusion_compat && no_prop > 0) src = ((no_prop - 1) % 2 == 0) ? st2 : st;
+    orc_spixl_to_image(V, W, H, S, spixl, labels, src, disp);
+  }
+  free(st);
+  free(st2);
+}
+
+/* detmath exports, so tests can check the pinned builtins against libm */
+double orc_dm_exp(double x) { return mvs_exp(x); }
+double orc_dm_log(double x) { return mvs_log(x); }
+float orc_dm_expf(float x) { return mvs_expf(x); }
+float orc_dm_powrf(float x, float y) { return mvs_powrf(x, y); }

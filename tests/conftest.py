@@ -1,0 +1,18 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libmvs.so on the GPU)")
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from cl_multiview_stereo_amd.engine import Engine
+    return Engine(0)

@@ -1,0 +1,251 @@
+"""GPU parity: the HIP path (libmvs.so through the C-ABI) against the CPU
+oracle (oracle/mvs_oracle.c) on the same seeded inputs.
+
+Bar: bit-exact for every stage -- labels, extents, disparities (integer-valued
+levels), Lab, superpixel statistics, NCC costs and refinement states -- because
+both sides evaluate the same pinned numerical definition (include/mvs_detmath.h,
+IEEE ops, no contraction).  Parity against the reference's own execution is
+UNPINNED (see oracle/mvs_oracle.c header and DESIGN.md).
+"""
+import numpy as np
+import pytest
+import torch
+
+from cl_multiview_stereo_amd import params, synth
+from cl_multiview_stereo_amd.engine import CameraArray
+from oracle import oracle as orc
+from tests.cases import CASES, PIXEL_CASES, as_u32, build
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def assert_bits(a, b, what):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if a.dtype.kind == "f":
+        eq = a.view(np.uint32 if a.dtype == np.float32 else np.uint64) == b.view(
+            np.uint32 if b.dtype == np.float32 else np.uint64)
+    else:
+        eq = a == b
+    bad = np.count_nonzero(~eq)
+    if bad:
+        idx = np.argwhere(~eq)[:5]
+        pytest.fail(f"{what}: {bad}/{a.size} elements differ; first at {idx.tolist()}: "
+                    f"{[a[tuple(i)] for i in idx]} vs {[b[tuple(i)] for i in idx]}")
+
+
+# ---------------------------------------------------------------------------
+def test_cvt_all_colours(engine):
+    # every (r, g, b) on a 4-step lattice plus the extremes, R/B swap included
+    v = np.arange(0, 256, 4, dtype=np.uint8)
+    r, g, b = np.meshgrid(v, v, v, indexing="ij")
+    rgbx = np.stack([r.ravel(), g.ravel(), b.ravel(), np.zeros(r.size, np.uint8)], -1)
+    rgbx = np.concatenate([rgbx, np.array([[255, 255, 255, 0], [0, 0, 0, 0], [255, 0, 0, 0]], np.uint8)])
+    W = 512
+    H = (len(rgbx) + W - 1) // W
+    pad = np.zeros((H * W - len(rgbx), 4), np.uint8)
+    img = np.concatenate([rgbx, pad]).reshape(1, H, W, 4)
+    lab, l8 = engine.cvt(dev(img))
+    want = orc.cvt(img[0])
+    assert_bits(lab.cpu().numpy()[0], want, "lab")
+    assert_bits(l8.cpu().numpy()[0], orc.l8(want), "l8")
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_slic(engine, name):
+    c = CASES[name]
+    b = build(c)
+    conn = name == "c2x2_s12"
+    lab, _ = engine.cvt(dev(b["stack"]))
+    sp, lb = engine.slic(lab, c["S"], 0.6, 5, conn)
+    sp, lb, lab = sp.cpu().numpy(), as_u32(lb), lab.cpu().numpy()
+    for v in range(b["V"]):
+        olab, osp, olb = orc.slic(b["stack"][v], c["S"], 0.6, 5, conn)
+        assert_bits(lab[v], olab, f"lab v{v}")
+        assert_bits(lb[v], olb, f"labels v{v}")
+        assert_bits(sp[v][..., :7], osp[..., :7], f"spixl v{v}")
+
+
+@pytest.mark.parametrize("name", ["c3x1_s8", "c5x1_s32"])
+def test_slic_each_pass(engine, name):
+    """Per-pass parity of the assign/update loop (no_iter = 0, 1, 2)."""
+    c = CASES[name]
+    b = build(c)
+    lab, _ = engine.cvt(dev(b["stack"][:1]))
+    for it in range(3):
+        sp, lb = engine.slic(lab, c["S"], 0.6, it)
+        _, osp, olb = orc.slic(b["stack"][0], c["S"], 0.6, it)
+        assert_bits(as_u32(lb)[0], olb, f"labels it{it}")
+        assert_bits(sp.cpu().numpy()[0][..., :7], osp[..., :7], f"spixl it{it}")
+
+
+def _chain(engine, c, b):
+    lab, _ = engine.cvt(dev(b["stack"]))
+    sp, lb = engine.slic(lab, c["S"], 0.6, 5)
+    rep = engine.boundary(sp, lb, c["S"])
+    return lab, sp, lb, rep
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_boundary_and_sweep(engine, name):
+    c = CASES[name]
+    b = build(c)
+    lab, sp, lb, rep = _chain(engine, c, b)
+    lab_h, sp_h, lb_h = lab.cpu().numpy(), sp.cpu().numpy(), as_u32(lb)
+    orep = orc.boundary(sp_h, lb_h, c["S"])
+    assert_bits(rep.cpu().numpy(), orep, "rep")
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
+    engine.sweep_spixl(lab, sp, rep, cam, c["S"])
+    osp = orc.sweep(lab_h, sp_h, orep, b["levels"], b["vs"], b["sn"], c["aw"], c["bl"], c["S"])
+    assert_bits(sp.cpu().numpy()[..., 7], osp[..., 7], "s7")
+
+
+@pytest.mark.parametrize("name", list(PIXEL_CASES))
+def test_grid_and_pixel_sad(engine, name):
+    c = PIXEL_CASES[name]
+    b = build(c)
+    lab, _ = engine.cvt(dev(b["stack"]))
+    sp, lb = engine.grid(lab, 1)
+    for v in range(b["V"]):
+        _, osp, olb = orc.grid(b["stack"][v], 1)
+        assert_bits(as_u32(lb)[v], olb, "grid labels")
+        assert_bits(sp.cpu().numpy()[v][..., :7], osp[..., :7], "grid spixl")
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
+    disp = engine.sweep_pixel_sad(lab, cam)
+    want = orc.sweep_pixel_sad(lab.cpu().numpy(), b["levels"], b["vs"], b["sn"], c["aw"], c["bl"])
+    assert_bits(disp.cpu().numpy(), want, "per-pixel SAD disparity")
+    # and the generic superpixel sweep on the S=1 grid gives the same map
+    rep = engine.boundary(sp, lb, 1)
+    engine.sweep_spixl(lab, sp, rep, cam, 1)
+    assert_bits(sp.cpu().numpy()[..., 7], want, "grid sweep == per-pixel sweep")
+
+
+@pytest.mark.parametrize("K", [5, 7])
+@pytest.mark.parametrize("name", ["c2x1_pix", "c2x2_pix", "c3x1_pix_odd", "c5x1_ncc"])
+def test_ncc_volume_and_wta(engine, name, K):
+    if name == "c5x1_ncc":
+        c = dict(aw=5, ah=1, W=150, H=70, dmin=0, dmax=20, bl=1.0, nh=4, nv=0, seed=23)
+    else:
+        c = PIXEL_CASES[name]
+    b = build(c)
+    lab, l8 = engine.cvt(dev(b["stack"]))
+    box = engine.box_stats(l8, K)
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
+    l8h = l8.cpu().numpy()
+    assert_bits(l8h, orc.l8(lab.cpu().numpy()), "l8")
+    lv = engine.levels_dev(cam)
+    for z in range(b["V"]):
+        vol = engine.ncc_volume(l8, box, cam, z, K)
+        want = orc.ncc_volume(l8h, b["levels"], b["vs"], b["sn"], c["aw"], c["bl"], K, z)
+        assert_bits(vol.cpu().numpy(), want, f"ncc volume z{z}")
+        disp, conf = engine.wta(vol, lv)
+        od, oc = orc.wta(want, b["levels"])
+        assert_bits(disp.cpu().numpy(), od, "wta disp")
+        assert_bits(conf.cpu().numpy(), oc, "wta conf")
+
+
+@pytest.mark.parametrize("name,ks", [("c3x3_s8", 26), ("c3x1_s16", 52), ("c5x1_s32", 1080), ("c3x1_s8", 1080)])
+def test_refinement(engine, name, ks):
+    c = CASES[name]
+    b = build(c)
+    lab, sp, lb, rep = _chain(engine, c, b)
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
+    engine.sweep_spixl(lab, sp, rep, cam, c["S"])
+    sp_h, lb_h, rep_h = sp.cpu().numpy(), as_u32(lb), rep.cpu().numpy()
+    want = orc.refine(sp_h, lb_h, rep_h, b["vs"], b["sn"], c["aw"], c["bl"], c["S"], 2.0, 6.0, 1.0, 13, ks, 5, True)
+    got = engine.refine(sp, lb, rep, cam, c["S"], 2.0, 6.0, 1.0, 13, ks, 5, True)
+    assert_bits(got["flat"].cpu().numpy(), want["flat"], "flatness")
+    assert_bits(got["state_compat"].cpu().numpy(), want["states"][3], "state after iteration 3 (fusion input)")
+    assert_bits(got["disp"].cpu().numpy(), want["disp"], "fused disparity")
+    # per-stage: init state and each propagate iteration
+    rp = params.refine_params(params.Settings(spixl_size=c["S"], kernel_size=ks))
+    flat = engine.flatness(sp, rp["flat_gamma"])
+    st = engine.init_state(sp, lb, rep, flat, cam, c["S"], rp["init_gamma"], rp["init_alpha"], rp["kernel_steps"],
+                           rp["kss"], rp["fuse"])
+    assert_bits(st.cpu().numpy(), want["state0"], "init state")
+    cur = st
+    for it in range(5):
+        nks, kss = params.prop_schedule(it, rp["kernel_steps"], rp["kss"])
+        nxt = torch.empty_like(cur)
+        engine.propagate(sp, lb, rep, flat, cam, c["S"], it, rp["prop_alpha"], rp["prop_gamma"], rp["fuse"], nks, kss,
+                         cur, nxt)
+        assert_bits(nxt.cpu().numpy(), want["states"][it], f"propagate iteration {it}")
+        cur = nxt
+
+
+@pytest.mark.parametrize("name", ["c3x3_s8", "c3x1_s16"])
+def test_filter(engine, name):
+    c = CASES[name]
+    b = build(c)
+    rng = np.random.default_rng(5)
+    V = b["V"]
+    disp = rng.integers(c["dmin"], c["dmax"] + 1, size=(V, c["H"], c["W"])).astype(np.float32)
+    disp[rng.random(disp.shape) < 0.05] = 0.0
+    disp += rng.choice(np.float32([0.0, 0.25, 0.5]), size=disp.shape)
+    proj, out = engine.filter(dev(disp), c["aw"], c["bl"], 1.0)
+    oproj, oout = orc.filt(disp, c["aw"], c["bl"], 1.0)
+    assert_bits(proj.cpu().numpy(), oproj, "filter projection")
+    assert_bits(out.cpu().numpy(), oout, "filter output")
+
+
+def test_determinism(engine):
+    c = CASES["c5x1_s32"]
+    b = build(c)
+    outs = []
+    for _ in range(2):
+        lab, sp, lb, rep = _chain(engine, c, b)
+        outs.append((sp.cpu().numpy().copy(), as_u32(lb).copy()))
+    assert_bits(outs[0][0], outs[1][0], "spixl rerun")
+    assert_bits(outs[0][1], outs[1][1], "labels rerun")
+
+
+def test_host_api_matches_device_api(engine):
+    """mvs_do_super_pixel_seg (host pointers) == device path."""
+    import ctypes as C
+    from cl_multiview_stereo_amd import _lib
+    c = CASES["c3x1_s16"]
+    b = build(c)
+    img = np.ascontiguousarray(b["stack"][0])
+    H, W = img.shape[:2]
+    mw, mh = params.map_size(W, H, c["S"])
+    lab = np.zeros((H, W, 4), np.float32)
+    sp = np.zeros((mh, mw, 8), np.float32)
+    lb = np.zeros((H, W), np.uint32)
+    p = _lib.SlicParams(c["S"], 0.6, 5, 0)
+    _lib.check(engine.L.mvs_do_super_pixel_seg(engine.ctx, img.ctypes.data_as(C.c_void_p), W, H, C.byref(p),
+                                               lab.ctypes.data_as(C.c_void_p), sp.ctypes.data_as(C.c_void_p),
+                                               lb.ctypes.data_as(C.c_void_p)), "mvs_do_super_pixel_seg")
+    olab, osp, olb = orc.slic(img, c["S"])
+    assert_bits(lb, olb, "host-API labels")
+    assert_bits(sp[..., :7], osp[..., :7], "host-API spixl")
+
+
+def test_bad_arguments_fail_loudly(engine):
+    from cl_multiview_stereo_amd import _lib
+    lab = torch.zeros((1, 16, 16, 4), device="cuda")
+    with pytest.raises(_lib.MvsError):
+        engine.slic(lab, 4)  # S < 6: the reference update divides by 3S/16 == 0
+
+
+def test_full_size_slic_properties(engine):
+    """1080p, S=32 (BASELINE config 2): labels in range, every label is one of
+    the pixel's candidate centres, and a rerun is bit-identical."""
+    stack, _ = synth.make_stack(1920, 1080, 5, 1, 0, 127, 1.0, 0x5EED + 2)
+    lab, _ = engine.cvt(dev(stack))
+    sp, lb = engine.slic(lab, 32)
+    sp2, lb2 = engine.slic(lab, 32)
+    assert torch.equal(lb, lb2) and torch.equal(sp, sp2)
+    lbh = as_u32(lb)
+    mw, mh = params.map_size(1920, 1080, 32)
+    assert lbh.max() < mw * mh
+    ys, xs = np.mgrid[0:1080, 0:1920]
+    lx, ly = lbh[0] % mw, lbh[0] // mw
+    assert np.all(np.abs(lx - xs // 32) <= 1) and np.all(np.abs(ly - ys // 32) <= 1)
+    # one view against the oracle at full size
+    olab, osp, olb = orc.slic(stack[0], 32)
+    assert_bits(lbh[0], olb, "1080p labels")

@@ -343,11 +343,23 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint8_t* __restrict__ 
       const bool xpin = xp >= R && xp < W - R;
       const uint8_t* Qv = q + (long)a.view[n] * P;
       const int2* Bv = box + (long)a.view[n] * P;
-      int hs[NR];
+      // issue every load of this (d, n) first: clamped addresses, no branches
+      int qpv[NR];
 #pragma unroll
       for (int k = 0; k < NR; k++) {
         int yy = min(max(yb - R + k - ty, 0), H - 1);
-        int p = qr[k] * (int)Qv[(long)yy * W + xpc];
+        qpv[k] = Qv[(long)yy * W + xpc];
+      }
+      int2 bp[TH];
+#pragma unroll
+      for (int o = 0; o < TH; o++) {
+        int yy = min(max(yb + o - ty, 0), H - 1);
+        bp[o] = Bv[(long)yy * W + xpc];
+      }
+      int hs[NR];
+#pragma unroll
+      for (int k = 0; k < NR; k++) {
+        int p = (int)__umul24(qr[k], qpv[k]);
         hs[k] = (K == 5) ? hsum5(p) : hsum7(p);
       }
       int srp = 0;
@@ -356,26 +368,19 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint8_t* __restrict__ 
 #pragma unroll
       for (int o = 0; o < TH; o++) {
         srp += hs[o + 2 * R];
-        const int y = yb + o;
-        const int yp = y - ty;
+        const int yp = yb + o - ty;
         const bool pin = xpin && yp >= R && yp < H - R;
-        float c;
-        if (!((rvalid >> o) & 1u) || !pin) {
-          c = 2.0f;
-        } else {
-          int2 b = Bv[(long)min(max(yp, 0), H - 1) * W + xpc];
-          int vp = NK * b.y - b.x * b.x;
-          if (!((rmask >> o) & 1u) || vp == 0) {
-            c = 1.0f;
-          } else {
-            int num = NK * srp - Sr[o] * b.x;
-            float fa = (float)num;
-            float bb = fa * fabsf(fa);
-            float cc = vrf[o] * (float)vp;
-            c = 1.0f - bb / cc;
-          }
-        }
-        if (c < mn[o]) mn[o] = c;
+        // all factors < 2^24: 24-bit multiplies are full rate (v_mul_u32_u24)
+        const int vp = NK * bp[o].y - (int)__umul24(bp[o].x, bp[o].x);
+        const int num = NK * srp - (int)__umul24(Sr[o], bp[o].x);
+        const float fa = (float)num;
+        const float bb = fa * fabsf(fa);
+        const float cc = vrf[o] * (float)vp;
+        const float cost = 1.0f - bb / cc;
+        const bool valid = ((rvalid >> o) & 1u) && pin;
+        const bool textured = ((rmask >> o) & 1u) && vp != 0;
+        const float c = !valid ? 2.0f : (!textured ? 1.0f : cost);
+        mn[o] = c < mn[o] ? c : mn[o];
         srp -= hs[o];
       }
     }

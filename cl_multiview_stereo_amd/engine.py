@@ -106,7 +106,8 @@ class Engine:
              spixl=None, labels=None):
         V, H, W, _ = lab.shape
         mw, mh = map_size(W, H, S)
-        spixl = self.empty((V, mh, mw, 8), torch.float32) if spixl is None else spixl
+        # s7 (disparity) is never written by SLIC (clcode.cl:285-293): start from zeros
+        spixl = torch.zeros((V, mh, mw, 8), dtype=torch.float32, device=self.device) if spixl is None else spixl
         labels = self.empty((V, H, W), torch.int32) if labels is None else labels
         if spixl.shape != (V, mh, mw, 8) or labels.shape != (V, H, W):
             raise ValueError("slic: output shapes do not match")

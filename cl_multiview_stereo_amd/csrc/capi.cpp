@@ -246,7 +246,7 @@ int mvs_ncc_volume_d(mvs_ctx* c, int W, int H, const uint8_t* l8, const int32_t*
   if (!c || !l8 || !box || !vol || bad_dims(W, H)) return mvs::arg_fail("mvs_ncc_volume_d: bad arguments");
   RC(upload_meta(c, a));
   if (z < 0 || z >= a->view_count) return mvs::arg_fail("mvs_ncc_volume_d: bad reference view");
-  return mvs::launch_ncc_volume(c->stream, a->view_count, W, H, l8, box, c->d_levels, a->num_levels,
+  return mvs::launch_ncc_volume(c->stream, a->view_count, W, H, l8, box, c->d_levels, a->levels, a->num_levels,
                                 a->view_subset, a->subset_num, a->array_width, a->bl_ratio, K, z, vol);
 }
 

@@ -10,11 +10,7 @@
 //                    in LDS as (c, a) pairs so the reference's
 //                    val+=30 / val-=30 / val+=AD sequence is three branch-free
 //                    adds per tap, summed in the reference's window order.
-//  k_box_stats       build-defined NCC: K x K window sums of l8 and l8^2
-//  k_ncc_volume      build-defined NCC K x K cost volume: one wave = 64 image
-//                    columns (64-2r outputs), rows slid in registers, the
-//                    horizontal K-sum of q_ref*q_nbr by DPP wave shifts, integer
-//                    sums (exact), IEEE f32 finish; cost = min over neighbours.
+//  (the NCC cost-volume kernels are in ncc.hip)
 //  k_wta             winner-take-all + confidence over the materialised volume
 //                    (the HBM-streaming pass the roofline is quoted on).
 #include "mvs_internal.h"
@@ -242,159 +238,6 @@ __global__ __launch_bounds__(256) void k_sweep_pixel_sad(const float4* __restric
   }
 }
 
-// ---- NCC: window sums of l8 / l8^2 ----------------------------------------
-__global__ void k_box_stats(const uint8_t* __restrict__ q, int W, int H, int K, int2* __restrict__ box) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
-  if (x >= W) return;
-  int r = K / 2;
-  long P = (long)W * H;
-  const uint8_t* Q = q + z * P;
-  int s = 0, ss = 0;
-  if (x - r >= 0 && x + r < W && y - r >= 0 && y + r < H) {
-    for (int j = -r; j <= r; j++)
-      for (int i = -r; i <= r; i++) {
-        int v = Q[(long)(y + j) * W + x + i];
-        s += v;
-        ss += v * v;
-      }
-  }
-  box[z * P + (long)y * W + x] = make_int2(s, ss);
-}
-
-// ---- NCC K x K cost volume -----------------------------------------------
-constexpr int kMaxNbr = 16;
-struct NccArgs {
-  int W, H, D, nn, z, d0, d1;
-  int view[kMaxNbr];
-  float fdx[kMaxNbr];  // dx as float
-  float fdy[kMaxNbr];  // dy as float
-  float bl;
-};
-
-__device__ __forceinline__ int hsum5(int p) {
-  // P(l-2)+P(l-1)+P(l)+P(l+1)+P(l+2) with DPP wave shifts (symmetric, exact)
-  int a1 = __builtin_amdgcn_update_dpp(0, p, 0x138, 0xf, 0xf, false);   // wave_shr:1
-  int a2 = __builtin_amdgcn_update_dpp(0, a1, 0x138, 0xf, 0xf, false);
-  int b1 = __builtin_amdgcn_update_dpp(0, p, 0x130, 0xf, 0xf, false);   // wave_shl:1
-  int b2 = __builtin_amdgcn_update_dpp(0, b1, 0x130, 0xf, 0xf, false);
-  return (((p + a1) + a2) + b1) + b2;
-}
-__device__ __forceinline__ int hsum7(int p) {
-  int a1 = __builtin_amdgcn_update_dpp(0, p, 0x138, 0xf, 0xf, false);
-  int a2 = __builtin_amdgcn_update_dpp(0, a1, 0x138, 0xf, 0xf, false);
-  int a3 = __builtin_amdgcn_update_dpp(0, a2, 0x138, 0xf, 0xf, false);
-  int b1 = __builtin_amdgcn_update_dpp(0, p, 0x130, 0xf, 0xf, false);
-  int b2 = __builtin_amdgcn_update_dpp(0, b1, 0x130, 0xf, 0xf, false);
-  int b3 = __builtin_amdgcn_update_dpp(0, b2, 0x130, 0xf, 0xf, false);
-  return (((((p + a1) + a2) + a3) + b1) + b2) + b3;
-}
-
-template <int K, int TH>
-__global__ __launch_bounds__(256) void k_ncc_volume(const uint8_t* __restrict__ q, const int2* __restrict__ box,
-                                                    const float* __restrict__ levels_dev, NccArgs a,
-                                                    float* __restrict__ vol) {
-  constexpr int R = K / 2;
-  constexpr int OUT = 64 - 2 * R;  // output columns per wave
-  constexpr int NR = TH + 2 * R;   // rows streamed per (d, n)
-  constexpr int NK = K * K;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int x = blockIdx.x * OUT - R + lane;
-  const int yb = (blockIdx.y * 4 + wave) * TH;
-  if (yb >= a.H) return;  // wave-uniform
-  const long P = (long)a.W * a.H;
-  const int W = a.W, H = a.H;
-  const int xc = min(max(x, 0), W - 1);
-  const uint8_t* Qz = q + (long)a.z * P;
-  // reference column, rows yb-R .. yb+TH+R-1
-  int qr[NR];
-#pragma unroll
-  for (int k = 0; k < NR; k++) {
-    int yy = min(max(yb - R + k, 0), H - 1);
-    qr[k] = Qz[(long)yy * W + xc];
-  }
-  const bool out_lane = lane >= R && lane < 64 - R && x < W;
-  const bool xin = x >= R && x < W - R;
-  int Sr[TH];
-  float vrf[TH];
-  unsigned rmask = 0;  // bit o: reference window valid and textured
-  unsigned rvalid = 0;
-#pragma unroll
-  for (int o = 0; o < TH; o++) {
-    int y = yb + o;
-    int yc = min(y, H - 1);
-    int2 b = box[(long)a.z * P + (long)yc * W + xc];
-    Sr[o] = b.x;
-    int vr = NK * b.y - b.x * b.x;
-    vrf[o] = (float)vr;
-    bool v = xin && y >= R && y < H - R;
-    rvalid |= (v ? 1u : 0u) << o;
-    rmask |= ((v && vr != 0) ? 1u : 0u) << o;
-  }
-  for (int dl = a.d0; dl < a.d1; dl++) {
-    const float d = levels_dev[dl];
-    float mn[TH];
-#pragma unroll
-    for (int o = 0; o < TH; o++) mn[o] = 1000000.0f;
-    for (int n = 0; n < a.nn; n++) {
-      const int tx = (int)roundf(d * a.fdx[n]);
-      const int ty = (int)roundf((a.bl * d) * a.fdy[n]);
-      const int xp = x - tx;
-      const int xpc = min(max(xp, 0), W - 1);
-      const bool xpin = xp >= R && xp < W - R;
-      const uint8_t* Qv = q + (long)a.view[n] * P;
-      const int2* Bv = box + (long)a.view[n] * P;
-      // issue every load of this (d, n) first: clamped addresses, no branches
-      int qpv[NR];
-#pragma unroll
-      for (int k = 0; k < NR; k++) {
-        int yy = min(max(yb - R + k - ty, 0), H - 1);
-        qpv[k] = Qv[(long)yy * W + xpc];
-      }
-      int2 bp[TH];
-#pragma unroll
-      for (int o = 0; o < TH; o++) {
-        int yy = min(max(yb + o - ty, 0), H - 1);
-        bp[o] = Bv[(long)yy * W + xpc];
-      }
-      int hs[NR];
-#pragma unroll
-      for (int k = 0; k < NR; k++) {
-        int p = (int)__umul24(qr[k], qpv[k]);
-        hs[k] = (K == 5) ? hsum5(p) : hsum7(p);
-      }
-      int srp = 0;
-#pragma unroll
-      for (int k = 0; k < 2 * R; k++) srp += hs[k];
-#pragma unroll
-      for (int o = 0; o < TH; o++) {
-        srp += hs[o + 2 * R];
-        const int yp = yb + o - ty;
-        const bool pin = xpin && yp >= R && yp < H - R;
-        // all factors < 2^24: 24-bit multiplies are full rate (v_mul_u32_u24)
-        const int vp = NK * bp[o].y - (int)__umul24(bp[o].x, bp[o].x);
-        const int num = NK * srp - (int)__umul24(Sr[o], bp[o].x);
-        const float fa = (float)num;
-        const float bb = fa * fabsf(fa);
-        const float cc = vrf[o] * (float)vp;
-        const float cost = 1.0f - bb / cc;
-        const bool valid = ((rvalid >> o) & 1u) && pin;
-        const bool textured = ((rmask >> o) & 1u) && vp != 0;
-        const float c = !valid ? 2.0f : (!textured ? 1.0f : cost);
-        mn[o] = c < mn[o] ? c : mn[o];
-        srp -= hs[o];
-      }
-    }
-    if (out_lane) {
-      float* vd = vol + (long)dl * P;
-#pragma unroll
-      for (int o = 0; o < TH; o++) {
-        int y = yb + o;
-        if (y < H) vd[(long)y * W + x] = mn[o];
-      }
-    }
-  }
-}
-
 // ---- winner-take-all + confidence ----------------------------------------
 __global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, const float* __restrict__ levels, long P,
                                              int D, float* __restrict__ disp, float* __restrict__ conf) {
@@ -483,50 +326,6 @@ int launch_sweep_pixel_sad(hipStream_t s, int V, int W, int H, const float* lab,
     hipLaunchKernelGGL(k_sweep_pixel_sad, dim3((W + PT - 1) / PT, (H + PT - 1) / PT), dim3(256), 0, s,
                        (const float4*)lab, levels, vs, sn, a, disp + (long)(z - z0) * P);
     MVS_LAUNCH_CHECK("k_sweep_pixel_sad");
-  }
-  return 0;
-}
-
-int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box) {
-  hipLaunchKernelGGL(k_box_stats, dim3((W + 255) / 256, H, V), dim3(256), 0, s, l8, W, H, K, (int2*)box);
-  MVS_LAUNCH_CHECK("k_box_stats");
-  return 0;
-}
-
-int launch_ncc_volume(hipStream_t s, int V, int W, int H, const uint8_t* l8, const int32_t* box,
-                      const float* levels_dev, int D, const int* vs_host, const int* sn_host, int aw, float bl,
-                      int K, int z, float* vol) {
-  constexpr int TH = 16;
-  NccArgs a{};
-  a.W = W; a.H = H; a.D = D; a.z = z; a.bl = bl;
-  a.nn = sn_host[z];
-  if (a.nn > kMaxNbr) return arg_fail("NCC sweep supports at most 16 neighbours per reference view");
-  int rx = z % aw, ry = z / aw;
-  for (int n = 0; n < a.nn; n++) {
-    int v = vs_host[V * z + n];
-    if (v < 0 || v >= V) return arg_fail("view_subset entry out of range");
-    a.view[n] = v;
-    a.fdx[n] = (float)(v % aw - rx);
-    a.fdy[n] = (float)(v / aw - ry);
-  }
-  if (K != 5 && K != 7) return arg_fail("NCC window must be 5 or 7");
-  int R = K / 2, OUT = 64 - 2 * R;
-  // split the hypotheses so the grid holds enough waves to fill 256 CUs
-  long tiles = (long)((W + OUT - 1) / OUT) * ((H + 4 * TH - 1) / (4 * TH));
-  int chunks = (int)((4096 + tiles - 1) / tiles);
-  if (chunks < 1) chunks = 1;
-  if (chunks > D) chunks = D;
-  int per = (D + chunks - 1) / chunks;
-  for (int c = 0; c < chunks; c++) {
-    a.d0 = c * per;
-    a.d1 = min(D, (c + 1) * per);
-    if (a.d0 >= a.d1) break;
-    dim3 g((W + OUT - 1) / OUT, (H + 4 * TH - 1) / (4 * TH));
-    if (K == 5)
-      hipLaunchKernelGGL((k_ncc_volume<5, TH>), g, dim3(256), 0, s, l8, (const int2*)box, levels_dev, a, vol);
-    else
-      hipLaunchKernelGGL((k_ncc_volume<7, TH>), g, dim3(256), 0, s, l8, (const int2*)box, levels_dev, a, vol);
-    MVS_LAUNCH_CHECK("k_ncc_volume");
   }
   return 0;
 }

@@ -334,10 +334,11 @@ void orc_sweep(int V, int W, int H, int S, const float* lab, float* spixl, const
 /*   q = L8 intensity; window K x K (r = K/2); shift (tx, ty) =             */
 /*   (roundf(d*dx), roundf((bl*d)*dy)); window valid iff every tap of the   */
 /*   reference and the shifted window lies inside the image.                */
-/*   num = n*Srp - Sr*Sp, vr = n*Srr - Sr^2, vp = n*Spp - Sp^2 (int32).     */
-/*   cost = 2 (invalid) | 1 (vr==0 or vp==0) | 1 - a*|a| / (vr_f * vp_f)    */
-/*   with a = (float)num.  cost(d) = min over neighbours (strict <, init    */
-/*   1e6); vol[z][d][y][x].                                                  */
+/*   num = n*Srp - Sr*Sp, vr = n*Srr - Sr^2, vp = n*Spp - Sp^2 (int32);     */
+/*   ivr = vr ? 1/(float)vr : 0, ivp likewise (per pixel, IEEE);            */
+/*   cost = 2 (invalid) | 1 - ((a*|a|)*ivr)*ivp with a = (float)num, i.e.   */
+/*   1 - signed squared NCC, 1 on textureless windows.                      */
+/*   cost(d) = min over neighbours (strict <, init 1e6); vol[d][y][x].      */
 /* ------------------------------------------------------------------------ */
 void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, int D, const int* vs,
                     const int* sn, int aw, float bl, int K, int z, float* vol) {
@@ -380,14 +381,13 @@ void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, 
               }
             int vp = nk * Spp - Sp * Sp;
             int num = nk * Srp - Sr * Sp;
-            if (vr == 0 || vp == 0) {
-              c = 1.0f;
-            } else {
-              float a = (float)num;
-              float bb = a * fabsf(a);
-              float cc = (float)vr * (float)vp;
-              c = 1.0f - bb / cc;
-            }
+            float ivr = vr != 0 ? 1.0f / (float)vr : 0.0f;
+            float ivp = vp != 0 ? 1.0f / (float)vp : 0.0f;
+            float a = (float)num;
+            float bb = a * fabsf(a);
+            float e = bb * ivr;
+            e = e * ivp;
+            c = 1.0f - e;
           }
           if (c < mn) mn = c;
         }

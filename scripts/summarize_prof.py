@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output (rocpd SQLite) into profiles/<tag>_*.
+
+    python scripts/summarize_prof.py <prof_dir> <tag>
+
+<prof_dir>/trace/*.db     --kernel-trace --stats   -> <tag>_kernel_stats.csv
+<prof_dir>/pmc_fetch/*.db --pmc FETCH_SIZE          \
+<prof_dir>/pmc_write/*.db --pmc WRITE_SIZE          -> <tag>_pmc.json, pmc_wta.json
+FETCH_SIZE on gfx950 counts 128-B requests at 64 B for wide coalesced streaming
+reads: it is doubled (MI355X_MICROARCH.md, HBM section).  WRITE_SIZE is exact
+for 16-B-per-lane streaming stores.
+"""
+import csv
+import glob
+import json
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def db(path):
+    f = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
+    return sqlite3.connect(f[0]) if f else None
+
+
+def short(name):
+    n = name.replace("mvs::(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0].strip()
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    c = db(os.path.join(src, "trace"))
+    rows = list(c.execute("select name,total_calls,total_duration,average,percentage from top_kernels"))
+    with open(os.path.join(out, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "total_us", "avg_us", "percent"])
+        for r in rows:
+            w.writerow([short(r[0]), r[1], round(r[2], 1), round(r[3], 1), round(r[4], 3)])
+    pmc = defaultdict(dict)
+    for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+        d = db(os.path.join(src, sub))
+        if d is None:
+            continue
+        acc = defaultdict(list)
+        for name, val in d.execute("select kernel_name, value from counters_collection where counter_name=?",
+                                   (counter,)):
+            acc[short(name)].append(val * 1024.0)  # counters are KB
+        for k, v in acc.items():
+            pmc[k][counter + "_bytes_per_launch"] = sum(v) / len(v)
+            pmc[k]["launches"] = len(v)
+    for k, v in pmc.items():
+        if "FETCH_SIZE_bytes_per_launch" in v:
+            v["hbm_read_bytes_corrected"] = 2.0 * v["FETCH_SIZE_bytes_per_launch"]
+        v["hbm_bytes_per_launch"] = v.get("hbm_read_bytes_corrected", 0.0) + v.get("WRITE_SIZE_bytes_per_launch", 0.0)
+    json.dump(pmc, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
+    if "k_wta" in pmc:
+        json.dump({"kernel": "k_wta", "source": f"profiles/{tag}_pmc.json",
+                   "hbm_bytes_per_launch": pmc["k_wta"]["hbm_bytes_per_launch"],
+                   "note": "2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes"},
+                  open(os.path.join(out, "pmc_wta.json"), "w"), indent=1)
+    for r in rows[:8]:
+        print(f"{short(r[0]):40s} calls={r[1]:5d} avg={r[3]:9.3f} us  {r[4]:6.2f}%")
+    for k in ("k_wta", "k_ncc_volume<5, 16>", "k_cvt", "k_update", "k_assign"):
+        if k in pmc:
+            print(k, {a: round(b / 1e6, 2) for a, b in pmc[k].items() if "bytes" in a})
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,222 @@
+"""View-sharded depth pipeline: one process per GPU, RCCL over xGMI.
+
+SURVEY.md 8(e).  The array's reference views are split into contiguous
+blocks, one block per rank (``view_block``).  The reference launches every
+stage over all views at once (photo_consistency.cpp:133, depth_refinement.cpp
+:738-889).  Each rank here runs the stages only for its block, and the ranks
+exchange exactly what later stages read from other views:
+
+  stage                             reads from other views    exchange
+  --------------------------------  ------------------------  ---------------------------
+  cvt (a1)                          -                         none (every rank holds the
+                                                              RGBx stack, converts all)
+  SLIC (a2-a6), own block           -                         all-gather spixl + labels
+  boundary (a8)                     -                         none (cheap, all views)
+  superpixel sweep (a9), own block  Lab of neighbours         all-gather spixl (s7 = seed)
+  per-pixel NCC + WTA, own block    l8 of neighbours          none until the filter
+  flatness / init state (a11-a12)   neighbours' s7 / labels   none (recomputed redundantly)
+  propagate (a13) x no_prop         neighbours' state         all-gather state every
+                                                              iteration (49 KB/view at S=32)
+  fusion (a14), own block           -                         -
+  cross-view filter (a15)           all disparity maps        ONE all-gather of disparity
+
+The backend does the compute for one rank: ``EngineBackend`` (HIP kernels
+through libmvs.so) on a GPU.  The tests substitute a CPU stand-in of the same
+interface, so that this orchestration runs under gloo with world_size 2.
+The collectives use ``all_gather_into_tensor``, which is RCCL on ROCm, for
+equal blocks, and fall back to list all-gather when blocks are ragged (or on
+gloo).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from . import params
+
+
+def view_block(V: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous balanced block [z0, z1) of reference views for `rank`: the
+    first V % world ranks take one extra view."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    base, extra = divmod(V, world)
+    z0 = rank * base + min(rank, extra)
+    return z0, z0 + base + (1 if rank < extra else 0)
+
+
+def all_blocks(V: int, world: int) -> list[tuple[int, int]]:
+    return [view_block(V, r, world) for r in range(world)]
+
+
+class ViewGather:
+    """All-gather of per-view blocks along dim 0 into a full [V, ...] tensor.
+
+    With equal blocks on an RCCL group this is one ``all_gather_into_tensor``
+    (in place when `full` is given).  Ragged blocks (V % world != 0) and gloo
+    use the list form."""
+
+    def __init__(self, V: int, group=None):
+        self.V = V
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.blocks = all_blocks(V, self.world)
+        self.equal = len({z1 - z0 for z0, z1 in self.blocks}) == 1
+        self.backend = dist.get_backend(group) if dist.is_initialized() else "none"
+
+    @property
+    def block(self) -> tuple[int, int]:
+        return self.blocks[self.rank]
+
+    def __call__(self, local: torch.Tensor, full: torch.Tensor | None = None) -> torch.Tensor:
+        z0, z1 = self.block
+        if local.shape[0] != z1 - z0:
+            raise ValueError(f"rank {self.rank}: local block has {local.shape[0]} views, expected {z1 - z0}")
+        shape = (self.V,) + tuple(local.shape[1:])
+        if full is None:
+            full = torch.empty(shape, dtype=local.dtype, device=local.device)
+        if self.world == 1:
+            if full.data_ptr() != local.data_ptr():
+                full.copy_(local)
+            return full
+        if self.equal and self.backend == "nccl":
+            src = local if local.is_contiguous() else local.contiguous()
+            dist.all_gather_into_tensor(full, src, group=self.group)
+            return full
+        n_max = max(b1 - b0 for b0, b1 in self.blocks)
+        pad_shape = (n_max,) + tuple(local.shape[1:])
+        send = torch.zeros(pad_shape, dtype=local.dtype, device=local.device)
+        send[:z1 - z0] = local
+        bufs = [torch.empty(pad_shape, dtype=local.dtype, device=local.device) for _ in range(self.world)]
+        dist.all_gather(bufs, send, group=self.group)
+        for (b0, b1), buf in zip(self.blocks, bufs):
+            full[b0:b1] = buf[:b1 - b0]
+        return full
+
+
+@dataclass
+class ShardOutput:
+    z0: int
+    z1: int
+    spixl: torch.Tensor                 # [V, mh, mw, 8] (gathered, s7 = seed disparity)
+    labels: torch.Tensor                # [V, H, W]      (gathered)
+    disp: torch.Tensor | None = None    # [z1-z0, H, W] per-pixel NCC/SAD disparity
+    conf: torch.Tensor | None = None
+    disp_refined: torch.Tensor | None = None   # [z1-z0, H, W]
+    disp_filtered: torch.Tensor | None = None  # [z1-z0, H, W]
+
+
+class ShardedPipeline:
+    """pipeline::perform_segmentation + perform_depth_est (pipeline.cpp:60-175)
+    over one rank's view block.  `backend` supplies the per-rank compute (see
+    EngineBackend for the interface)."""
+
+    def __init__(self, backend, settings: params.Settings, cam, gather: ViewGather,
+                 pixel_cost: str | None = "ncc", refine: bool = True, filt: bool = True):
+        self.b, self.st, self.cam, self.g = backend, settings, cam, gather
+        self.pixel_cost, self.refine, self.filt = pixel_cost, refine, filt
+
+    def run(self, rgbx: torch.Tensor) -> ShardOutput:
+        st, b, g = self.st, self.b, self.g
+        V = rgbx.shape[0]
+        if V != g.V:
+            raise ValueError("stack size does not match the gather's view count")
+        z0, z1 = g.block
+        S = st.spixl_size
+        lab, l8 = b.cvt(rgbx)
+        sp_blk, lb_blk = b.slic(lab[z0:z1], S, st.slic_color_weight, st.no_iter, st.enforce_connectivity)
+        spixl = g(sp_blk)
+        labels = g(lb_blk)
+        rep = b.boundary(spixl, labels, S)
+        b.sweep_spixl(lab, spixl, rep, self.cam, S, z0, z1)
+        spixl = g(spixl[z0:z1].contiguous(), spixl)
+        out = ShardOutput(z0, z1, spixl, labels)
+        if self.pixel_cost:
+            out.disp, out.conf = b.pixel_sweep(lab, l8, self.cam, z0, z1, self.pixel_cost, st.window)
+        if self.refine:
+            out.disp_refined = self._refine(spixl, labels, rep, z0, z1)
+        if self.filt:
+            src = out.disp_refined if out.disp_refined is not None else out.disp
+            full = g(src)
+            out.disp_filtered = b.filter(full, st.array_width, st.bl_ratio, st.fuse, z0, z1)[z0:z1]
+        return out
+
+    def _refine(self, spixl, labels, rep, z0, z1):
+        """clDepthRefinement::do_refinement (depth_refinement.cpp:91-118, 724-889)
+        with the Jacobi ping-pong of mvs_refine_d; each iteration's output block
+        is all-gathered before the next iteration reads it."""
+        st, b, g = self.st, self.b, self.g
+        rp = params.refine_params(st)
+        flat = b.flatness(spixl, rp["flat_gamma"])
+        state = b.init_state(spixl, labels, rep, flat, self.cam, st.spixl_size, rp["init_gamma"], rp["init_alpha"],
+                             rp["kernel_steps"], rp["kss"], rp["fuse"])
+        state2 = state.clone()
+        for it in range(st.no_prop):
+            src, dst = (state, state2) if it % 2 == 0 else (state2, state)
+            nks, kss = params.prop_schedule(it, rp["kernel_steps"], rp["kss"])
+            b.propagate(spixl, labels, rep, flat, self.cam, st.spixl_size, it, rp["prop_alpha"], rp["prop_gamma"],
+                        rp["fuse"], nks, kss, src, dst, z0, z1)
+            g(dst[z0:z1].contiguous(), dst)
+        # fusion renders current_state_dev = `state` (Appendix A #13)
+        return b.spixl_to_image(spixl[z0:z1], labels[z0:z1], state[z0:z1], st.spixl_size)
+
+
+class EngineBackend:
+    """Per-rank compute on the GPU through libmvs.so (Engine)."""
+
+    def __init__(self, engine):
+        self.e = engine
+
+    def cvt(self, rgbx):
+        return self.e.cvt(rgbx, want_l8=True)
+
+    def slic(self, lab_blk, S, weight, no_iter, conn):
+        if S == 1:
+            return self.e.grid(lab_blk, 1)
+        return self.e.slic(lab_blk, S, weight, no_iter, conn)
+
+    def boundary(self, spixl, labels, S):
+        return self.e.boundary(spixl, labels, S)
+
+    def sweep_spixl(self, lab, spixl, rep, cam, S, z0, z1):
+        self.e.sweep_spixl(lab, spixl, rep, cam, S, z0, z1)
+
+    def pixel_sweep(self, lab, l8, cam, z0, z1, cost, K):
+        from .pipeline import PixelSweep
+        H, W = lab.shape[1:3]
+        return PixelSweep(self.e, cam, W, H, cost, K).run(lab, l8, z0, z1)
+
+    def flatness(self, spixl, gamma):
+        return self.e.flatness(spixl, gamma)
+
+    def init_state(self, *a):
+        return self.e.init_state(*a)
+
+    def propagate(self, *a):
+        return self.e.propagate(*a)
+
+    def spixl_to_image(self, spixl, labels, state, S):
+        return self.e.spixl_to_image(spixl.contiguous(), labels.contiguous(), state.contiguous(), S)
+
+    def filter(self, disp_full, aw, bl, fuse, z0, z1):
+        return self.e.filter(disp_full, aw, bl, fuse, z0, z1)[1]
+
+
+def init_from_env(backend: str = "nccl"):
+    """torch.distributed init for `torch.distributed.run` launches (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT from the environment)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return rank, world, local

@@ -243,3 +243,50 @@ def filt(disp_full, array_width, bl_ratio, fuse=1.0):
     lib().orc_filter(V, W, H, array_width, _f(bl_ratio), _f(0.5 * fuse), _p(df, f32p), _p(proj, f32p),
                      _p(out, f32p))
     return proj, out
+
+
+def flatness(spixl, gamma):
+    spixl = np.ascontiguousarray(spixl, np.float32)
+    V, mh, mw, _ = spixl.shape
+    flat = np.zeros((V, mh, mw, 2), np.float32)
+    lib().orc_flatness(V, mw, mh, _p(spixl, f32p), _f(gamma), _p(flat, f32p))
+    return flat
+
+
+def init_state(spixl, labels, rep, flat, view_subset, subset_num, array_width, bl_ratio, S, gamma, alpha, nks, kss,
+               fuse):
+    """init_current_state with the kernel-side scalars (1/gamma', 1/alpha', fuse/2)."""
+    spixl = np.ascontiguousarray(spixl, np.float32)
+    labels = np.ascontiguousarray(labels, np.uint32)
+    rep = np.ascontiguousarray(rep, np.uint8)
+    flat = np.ascontiguousarray(flat, np.float32)
+    vs = np.ascontiguousarray(view_subset, np.int32)
+    sn = np.ascontiguousarray(subset_num, np.int32)
+    V, H, W = labels.shape
+    mw, mh = map_size(W, H, S)
+    st = np.zeros((V, mh, mw, 6), np.float32)
+    lib().orc_init_state(V, W, H, S, array_width, _f(bl_ratio), _p(spixl, f32p), _p(labels, u32p), _p(rep, u8p),
+                         _p(flat, f32p), _p(vs, i32p), _p(sn, i32p), _f(gamma), _f(alpha), int(nks), _f(kss),
+                         _f(fuse), _p(st, f32p))
+    return st
+
+
+def suppress(labels):
+    """supress_local_lable, one pass."""
+    labels = np.ascontiguousarray(labels, np.uint32)
+    H, W = labels.shape
+    out = np.zeros_like(labels)
+    lib().orc_suppress(_p(labels, u32p), _p(out, u32p), W, H)
+    return out
+
+
+def slic_from_lab(lab, S, weight=0.6, no_iter=5, enforce_connectivity=False):
+    """clSLIC::do_super_pixel_seg minus its cvt, on one view's Lab."""
+    sp = init_centers(lab, S)
+    lb = assign(lab, sp, S, weight)
+    for _ in range(no_iter):
+        sp = update(lab, lb, S)
+        lb = assign(lab, sp, S, weight)
+    if enforce_connectivity:
+        lb = suppress(suppress(lb))
+    return sp, lb

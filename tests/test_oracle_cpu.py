@@ -1,0 +1,229 @@
+"""CPU suite: the C oracle against the independent numpy restatement
+(tests/np_ref.py), the pinned math kernels against libm, and known answers.
+
+No GPU needed.  Sizes keep the whole file to a few seconds.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+import oracle.oracle as orc
+from cases import CASES, PIXEL_CASES, build
+from np_ref import (assign, boundary, cvt_f64, grid_labels, l8, ncc_volume, suppress, sweep_pixel_sad, update,
+                    wta)
+
+
+@pytest.fixture(scope="module", params=["c3x3_s8", "c2x2_s12", "c3x1_s16"])
+def slic_case(request):
+    c = CASES[request.param]
+    b = build(c)
+    return c, b
+
+
+# ---------------------------------------------------------------- detmath ---
+def test_detmath_exp_log_close_to_libm():
+    xs = np.concatenate([np.linspace(-700, 700, 2001), np.linspace(-1, 1, 2001), [0.0, 1e-300, -1e-300]])
+    for x in xs:
+        e = orc.lib().orc_dm_exp
+        e.restype = __import__("ctypes").c_double
+        e.argtypes = [__import__("ctypes").c_double]
+        ref = math.exp(x)
+        got = e(x)
+        assert abs(got - ref) <= 4e-16 * ref + 1e-320, (x, got, ref)
+    lg = orc.lib().orc_dm_log
+    lg.restype = __import__("ctypes").c_double
+    lg.argtypes = [__import__("ctypes").c_double]
+    for x in np.concatenate([np.geomspace(1e-300, 1e300, 1001), np.linspace(0.5, 2, 1001)]):
+        assert abs(lg(x) - math.log(x)) <= 4e-16 * max(1.0, abs(math.log(x))), x
+
+
+def test_detmath_powr_cube_root():
+    import ctypes as C
+    pw = orc.lib().orc_dm_powrf
+    pw.restype = C.c_float
+    pw.argtypes = [C.c_float, C.c_float]
+    third = np.float32(1.0) / np.float32(3.0)
+    for x in np.linspace(0.008857, 1.2, 997, dtype=np.float32):
+        got = pw(float(x), float(third))
+        ref = float(np.float32(float(x) ** float(third)))
+        assert abs(got - ref) <= 2 * np.spacing(np.float32(ref)), (x, got, ref)
+    assert pw(0.0, float(third)) == 0.0
+
+
+def test_detmath_expf():
+    import ctypes as C
+    ef = orc.lib().orc_dm_expf
+    ef.restype = C.c_float
+    ef.argtypes = [C.c_float]
+    for x in np.linspace(-80, 80, 4001, dtype=np.float32):
+        ref = np.float32(math.exp(float(x)))
+        got = np.float32(ef(float(x)))
+        assert abs(float(got) - float(ref)) <= float(np.spacing(ref)), (x, got, ref)
+
+
+# ------------------------------------------------------------- colour/grid ---
+def test_cvt_known_answers():
+    px = np.array([[[255, 255, 255, 0], [0, 0, 0, 0], [0, 0, 255, 0], [255, 0, 0, 0]]], np.uint8)
+    lab = orc.cvt(px)
+    assert abs(lab[0, 0, 0] - 100.0) < 0.01 and abs(lab[0, 0, 1]) < 0.05 and abs(lab[0, 0, 2]) < 0.05
+    assert lab[0, 1, 0] == 0.0 and lab[0, 1, 1] == 0.0 and lab[0, 1, 2] == 0.0
+    # R/B swap: s2 is RED in the reference's reading (rgb2lab(s0=B,...))
+    assert abs(lab[0, 2, 0] - 53.24) < 0.05 and lab[0, 2, 1] > 75
+    assert abs(lab[0, 3, 0] - 32.30) < 0.05 and lab[0, 3, 2] < -100
+
+
+def test_cvt_matches_f64_model():
+    rng = np.random.default_rng(3)
+    px = rng.integers(0, 256, (37, 53, 4), dtype=np.uint8)
+    lab = orc.cvt(px)
+    ref = cvt_f64(px)
+    np.testing.assert_allclose(lab[..., :3], ref, atol=2e-3)
+    assert (lab[..., 3] == 0).all()
+
+
+def test_l8_bit_exact():
+    rng = np.random.default_rng(4)
+    lab = np.zeros((31, 47, 4), np.float32)
+    lab[..., 0] = rng.uniform(-5, 110, (31, 47)).astype(np.float32)
+    lab[0, :4, 0] = [0.0, 99.99, 100.0, 100.0 / 2.55]
+    assert np.array_equal(orc.l8(lab), l8(lab))
+
+
+@pytest.mark.parametrize("W,H,S", [(100, 70, 8), (37, 29, 1), (250, 170, 40), (64, 64, 16)])
+def test_grid_labels(W, H, S):
+    _, sp, lb = orc.grid(np.zeros((H, W, 4), np.uint8), S)
+    assert np.array_equal(lb, grid_labels(W, H, S))
+    mw, mh = orc.map_size(W, H, S)
+    assert sp.shape == (mh, mw, 8) and lb.max() < mw * mh
+
+
+# ------------------------------------------------------------------- SLIC ---
+def test_assign_bit_exact(slic_case):
+    c, b = slic_case
+    S = c["S"]
+    lab = orc.cvt(b["stack"][0])
+    sp = orc.init_centers(lab, S)
+    assert np.array_equal(orc.assign(lab, sp, S), assign(lab, sp, S))
+
+
+def test_update_bit_exact(slic_case):
+    c, b = slic_case
+    S = c["S"]
+    lab = orc.cvt(b["stack"][1])
+    lb = orc.assign(lab, orc.init_centers(lab, S), S)
+    got = orc.update(lab, lb, S)
+    ref = update(lab, lb, S)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_slic_pipeline_bit_exact(slic_case):
+    """do_super_pixel_seg = init, assign, (update, assign) x no_iter."""
+    c, b = slic_case
+    S = c["S"]
+    lab, sp, lb = orc.slic(b["stack"][0], S, no_iter=3)
+    l2 = orc.cvt(b["stack"][0])
+    s2 = orc.init_centers(l2, S)
+    b2 = assign(l2, s2, S)
+    for _ in range(3):
+        s2 = update(l2, b2, S)
+        b2 = assign(l2, s2, S)
+    assert np.array_equal(lb, b2)
+    assert np.array_equal(sp.view(np.uint32), s2.view(np.uint32))
+
+
+def test_slic_invariants(slic_case):
+    c, b = slic_case
+    S, W, H = c["S"], c["W"], c["H"]
+    _, sp, lb = orc.slic(b["stack"][0], S)
+    mw, mh = orc.map_size(W, H, S)
+    assert lb.max() < mw * mh
+    # every pixel's label is one of the 2x2 candidate centres around its cell
+    y, x = np.mgrid[0:H, 0:W]
+    lx, ly = lb % mw, lb // mw
+    assert (np.abs(lx.astype(int) - x // S) <= 1).all() and (np.abs(ly.astype(int) - y // S) <= 1).all()
+    # ids, counts
+    assert np.array_equal(sp[..., 0].reshape(-1), np.arange(mw * mh, dtype=np.float32))
+    n = sp[..., 6]
+    assert (n >= 0).all() and n.sum() <= W * H
+
+
+def test_enforce_connectivity_bit_exact(slic_case):
+    c, b = slic_case
+    S = c["S"]
+    _, _, lb0 = orc.slic(b["stack"][2 % b["V"]], S)
+    _, _, lb1 = orc.slic(b["stack"][2 % b["V"]], S, enforce_connectivity=True)
+    assert np.array_equal(lb1, suppress(suppress(lb0)))
+
+
+# --------------------------------------------------------- sweep / boundary ---
+def test_boundary_bit_exact(slic_case):
+    c, b = slic_case
+    S = c["S"]
+    outs = [orc.slic(b["stack"][v], S) for v in range(b["V"])]
+    sp = np.stack([o[1] for o in outs])
+    lb = np.stack([o[2] for o in outs])
+    assert np.array_equal(orc.boundary(sp, lb, S), boundary(sp, lb, S))
+
+
+@pytest.mark.parametrize("name", list(PIXEL_CASES))
+def test_sweep_pixel_sad_bit_exact(name):
+    c = PIXEL_CASES[name]
+    b = build(c)
+    lab = orc.cvt(b["stack"])
+    lv = b["levels"][:8]
+    got = orc.sweep_pixel_sad(lab, lv, b["vs"], b["sn"], c["aw"], c["bl"])
+    ref = sweep_pixel_sad(lab, lv, b["vs"], b["sn"], c["aw"], c["bl"])
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,K", [("c2x1_pix", 5), ("c2x2_pix", 5), ("c3x1_pix_odd", 7), ("c2x2_pix", 3)])
+def test_ncc_volume_bit_exact(name, K):
+    c = PIXEL_CASES[name]
+    b = build(c)
+    q = orc.l8(orc.cvt(b["stack"]))
+    for z in range(b["V"]):
+        got = orc.ncc_volume(q, b["levels"], b["vs"], b["sn"], c["aw"], c["bl"], K, z)
+        ref = ncc_volume(q, b["levels"], b["vs"], b["sn"], c["aw"], c["bl"], K, z)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), z
+
+
+def test_ncc_cost_range_and_identity():
+    """Costs lie in [0, 2]; a view matched against an identical neighbour at
+    zero shift costs 1 - 1 = 0 wherever it is textured."""
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 256, (32, 40), dtype=np.uint8)
+    q = np.stack([img, img])
+    vs = np.array([[1, 0], [0, 0]], np.int32)
+    sn = np.array([1, 1], np.int32)
+    vol = orc.ncc_volume(q, np.array([0, 1, 2], np.float32), vs, sn, 2, 1.0, 5, 0)
+    assert vol.min() >= -1e-6 and vol.max() <= 2  # e = (a|a|/vr)/vp rounds to 1+ulp
+    inner = vol[0, 2:-2, 2:-2]
+    assert np.allclose(inner, 0, atol=1e-6)
+    assert (vol[0, :2] == 2).all() and (vol[0, :, :2] == 2).all()
+
+
+def test_wta_bit_exact_with_ties():
+    rng = np.random.default_rng(9)
+    vol = rng.integers(0, 6, (17, 23, 29)).astype(np.float32) * np.float32(0.25)
+    vol[:, 0, 0] = 1e6  # all-invalid pixel keeps disparity 0
+    lv = np.arange(17, dtype=np.float32) * 2 + 1
+    d0, c0 = orc.wta(vol, lv)
+    d1, c1 = wta(vol, lv)
+    assert np.array_equal(d0, d1) and np.array_equal(c0, c1)
+    assert d0[0, 0] == 0 and c0[0, 0] == 0
+
+
+def test_sweep_recovers_planar_disparity():
+    """End-to-end sanity of the oracle: NCC+WTA on a rendered fronto-parallel
+    stack recovers most of the ground-truth disparity."""
+    c = PIXEL_CASES["c2x1_pix"]
+    b = build(c)
+    q = orc.l8(orc.cvt(b["stack"]))
+    vol = orc.ncc_volume(q, b["levels"], b["vs"], b["sn"], c["aw"], c["bl"], 5, 0)
+    d, _ = orc.wta(vol, b["levels"])
+    gt = b["gt"][0] if b["gt"].ndim == 3 else b["gt"]
+    inner = (slice(4, -4), slice(int(c["dmax"]) + 4, -4))
+    assert np.mean(np.abs(d[inner] - gt[inner]) <= 1) > 0.6

@@ -101,6 +101,29 @@ int arg_fail(const char* what) {
   g_err = what;
   return MVS_E_ARG;
 }
+const int32_t* plan_upload(mvs_ctx* ctx, const std::vector<int32_t>& table, int* rc) {
+  *rc = 0;
+  auto it = ctx->plans.find(table);
+  if (it != ctx->plans.end()) return it->second;
+  if (ctx->plans.size() >= 256) {  // bound the cache: drop everything once in-flight work is done
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) { *rc = hip_fail(hipGetLastError(), "plan sync"); return nullptr; }
+    for (auto& kv : ctx->plans) hipFree(kv.second);
+    ctx->plans.clear();
+  }
+  int32_t* d = nullptr;
+  size_t bytes = sizeof(int32_t) * (table.empty() ? 1 : table.size());
+  if (hipMalloc(&d, bytes) != hipSuccess) {
+    set_error("plan allocation failed");
+    *rc = MVS_E_NOMEM;
+    return nullptr;
+  }
+  auto ins = ctx->plans.emplace(table, d).first;  // the map's key is the (stable) copy source
+  hipError_t e = hipMemcpyAsync(d, ins->first.data(), sizeof(int32_t) * table.size(), hipMemcpyHostToDevice,
+                                ctx->stream);
+  if (e != hipSuccess) { *rc = hip_fail(e, "plan upload"); return nullptr; }
+  return d;
+}
+
 void* scratch(mvs_ctx* ctx, size_t bytes, int* rc) {
   *rc = 0;
   if (ctx->scratch_bytes >= bytes && ctx->scratch) return ctx->scratch;
@@ -151,6 +174,7 @@ void mvs_destroy(mvs_ctx* c) {
   if (c->d_levels) hipFree(c->d_levels);
   if (c->d_vs) hipFree(c->d_vs);
   if (c->d_sn) hipFree(c->d_sn);
+  for (auto& kv : c->plans) hipFree(kv.second);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -246,8 +270,8 @@ int mvs_ncc_volume_d(mvs_ctx* c, int W, int H, const uint8_t* l8, const int32_t*
   if (!c || !l8 || !box || !vol || bad_dims(W, H)) return mvs::arg_fail("mvs_ncc_volume_d: bad arguments");
   RC(upload_meta(c, a));
   if (z < 0 || z >= a->view_count) return mvs::arg_fail("mvs_ncc_volume_d: bad reference view");
-  return mvs::launch_ncc_volume(c->stream, a->view_count, W, H, l8, box, c->d_levels, a->levels, a->num_levels,
-                                a->view_subset, a->subset_num, a->array_width, a->bl_ratio, K, z, vol);
+  return mvs::launch_ncc_volume(c, a->view_count, W, H, box, a->levels, a->num_levels, a->view_subset,
+                                a->subset_num, a->array_width, a->bl_ratio, K, z, vol);
 }
 
 int mvs_wta_d(mvs_ctx* c, int W, int H, int D, const float* vol, const float* levels, float* disp, float* conf) {

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -25,6 +26,9 @@ struct mvs_ctx {
   size_t cap_levels = 0, cap_vs = 0, cap_sn = 0;
   std::vector<float> h_levels;
   std::vector<int> h_vs, h_sn;
+  // small host-built launch plans (e.g. the NCC shift tables), uploaded once
+  // per distinct content and kept for the life of the context
+  std::map<std::vector<int32_t>, int32_t*> plans;
 };
 
 namespace mvs {
@@ -33,6 +37,7 @@ void set_error(const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
 int arg_fail(const char* what);
 void* scratch(mvs_ctx* ctx, size_t bytes, int* rc);
+const int32_t* plan_upload(mvs_ctx* ctx, const std::vector<int32_t>& table, int* rc);
 
 inline int map_dim(int n, int S) {
   // (int)ceil((float)n / (float)S), pipeline.cpp:18-19
@@ -72,9 +77,8 @@ int launch_sweep_pixel_sad(hipStream_t s, int V, int W, int H, const float* lab,
                            const int* vs, const int* sn, const int* sn_host, int aw, float bl, int z0, int z1,
                            float* disp);
 int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box);
-int launch_ncc_volume(hipStream_t s, int V, int W, int H, const uint8_t* l8, const int32_t* box,
-                      const float* levels_dev, const float* levels_host, int D, const int* vs_host,
-                      const int* sn_host, int aw, float bl, int K, int z, float* vol);
+int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
+                      const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol);
 int launch_wta(hipStream_t s, int W, int H, int D, const float* vol, const float* levels, float* disp,
                float* conf);
 

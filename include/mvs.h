@@ -115,10 +115,13 @@ int mvs_sweep_spixl_d(mvs_ctx* ctx, int W, int H, int S, const float* lab, float
 int mvs_sweep_pixel_sad_d(mvs_ctx* ctx, int W, int H, const float* lab, const mvs_array* a, int z0, int z1,
                           float* disp);
 
-/* Build-defined per-pixel NCC KxK plane sweep.  box [2][V][H][W] planar
- * per-pixel window statistics of l8 (mvs_box_stats_d): plane 0 S = sum q
- * (int32), plane 1 (float) 1/(n*sum q^2 - S^2) or 0 if textureless; vol
- * [D][H][W] float cost of reference view z (definition: csrc/ncc.hip). */
+/* Build-defined per-pixel NCC KxK plane sweep (definition: csrc/ncc.hip).
+ * box int32 [2][V][H][W][2] (16 B/px, from mvs_box_stats_d): plane 0 per-pixel
+ * window statistics {S = sum q, bits(1/(n*sum q^2 - S^2)) (0 if textureless,
+ * NaN if the window leaves the image)}; plane 1 the packed intensities
+ * q(x-R .. x-R+7) of each pixel's row (two little-endian dwords).
+ * vol [D][H][W] float cost of reference view z = 1 - max(-1, best signed
+ * squared NCC over valid neighbour windows); l8 is validated only. */
 int mvs_box_stats_d(mvs_ctx* ctx, const uint8_t* l8, int V, int W, int H, int K, int32_t* box);
 int mvs_ncc_volume_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
                      int K, int z, float* vol);

@@ -336,9 +336,9 @@ void orc_sweep(int V, int W, int H, int S, const float* lab, float* spixl, const
 /*   reference and the shifted window lies inside the image.                */
 /*   num = n*Srp - Sr*Sp, vr = n*Srr - Sr^2, vp = n*Spp - Sp^2 (int32);     */
 /*   ivr = vr ? 1/(float)vr : 0, ivp likewise (per pixel, IEEE);            */
-/*   cost = 2 (invalid) | 1 - ((a*|a|)*ivr)*ivp with a = (float)num, i.e.   */
-/*   1 - signed squared NCC, 1 on textureless windows.                      */
-/*   cost(d) = min over neighbours (strict <, init 1e6); vol[d][y][x].      */
+/*   e = ((a*|a|)*ivr)*ivp with a = (float)num: the signed squared NCC (0   */
+/*   on textureless windows); E = max(-1, max over VALID neighbours of e);  */
+/*   vol[d][y][x] = 1 - E  (2 when no neighbour window is valid).           */
 /* ------------------------------------------------------------------------ */
 void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, int D, const int* vs,
                     const int* sn, int aw, float bl, int K, int z, float* vol) {
@@ -360,38 +360,33 @@ void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, 
       int vr = nk * Srr - Sr * Sr;
       for (int dl = 0; dl < D; dl++) {
         float d = levels[dl];
-        float mn = 1000000.0f;
+        float best = -1.0f;
         for (int n = 0; n < sn[z]; n++) {
           int view = vs[V * z + n];
           int dx = view % aw - rx, dy = view / aw - ry;
           int tx = (int)roundf(d * (float)dx);
           int ty = (int)roundf((bl * d) * (float)dy);
           int px = x - tx, py = y - ty;
-          float c;
-          if (!rin || px - r < 0 || px + r >= W || py - r < 0 || py + r >= H) {
-            c = 2.0f;
-          } else {
-            const uint8_t* qp = q + (long)view * P;
-            int Sp = 0, Spp = 0, Srp = 0;
-            for (int j = -r; j <= r; j++)
-              for (int i = -r; i <= r; i++) {
-                int a = qr[(long)(y + j) * W + x + i];
-                int b = qp[(long)(py + j) * W + px + i];
-                Sp += b; Spp += b * b; Srp += a * b;
-              }
-            int vp = nk * Spp - Sp * Sp;
-            int num = nk * Srp - Sr * Sp;
-            float ivr = vr != 0 ? 1.0f / (float)vr : 0.0f;
-            float ivp = vp != 0 ? 1.0f / (float)vp : 0.0f;
-            float a = (float)num;
-            float bb = a * fabsf(a);
-            float e = bb * ivr;
-            e = e * ivp;
-            c = 1.0f - e;
-          }
-          if (c < mn) mn = c;
+          if (!rin || px - r < 0 || px + r >= W || py - r < 0 || py + r >= H) continue;
+          const uint8_t* qp = q + (long)view * P;
+          int Sp = 0, Spp = 0, Srp = 0;
+          for (int j = -r; j <= r; j++)
+            for (int i = -r; i <= r; i++) {
+              int a = qr[(long)(y + j) * W + x + i];
+              int b = qp[(long)(py + j) * W + px + i];
+              Sp += b; Spp += b * b; Srp += a * b;
+            }
+          int vp = nk * Spp - Sp * Sp;
+          int num = nk * Srp - Sr * Sp;
+          float ivr = vr != 0 ? 1.0f / (float)vr : 0.0f;
+          float ivp = vp != 0 ? 1.0f / (float)vp : 0.0f;
+          float a = (float)num;
+          float e = a * fabsf(a);
+          e = e * ivr;
+          e = e * ivp;
+          if (e > best) best = e;
         }
-        vol[((long)dl * H + y) * W + x] = mn;
+        vol[((long)dl * H + y) * W + x] = 1.0f - best;
       }
     }
 }

@@ -228,7 +228,8 @@ def _box(a, r):
 
 
 def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
-    """Build-defined NCC K x K cost volume (csrc/ncc.hip header) -> [D][H][W]."""
+    """Build-defined NCC K x K cost volume (csrc/ncc.hip header) -> [D][H][W]:
+    1 - max(-1, max over valid neighbour windows of the signed squared NCC)."""
     V, H, W = q.shape
     r, nk = K // 2, K * K
     bl = f32(bl)
@@ -244,7 +245,7 @@ def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
     rin = (x - r >= 0) & (x + r < W) & (y - r >= 0) & (y + r < H)
     vol = np.zeros((len(levels), H, W), f32)
     for dl, d in enumerate(np.asarray(levels, f32)):
-        mn = np.full((H, W), f32(1e6), f32)
+        best = np.full((H, W), f32(-1), f32)
         for n in range(sn[z]):
             view = vs[z, n]
             dx, dy = view % aw - rx, view // aw - ry
@@ -270,9 +271,8 @@ def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
             a = (nk * Srp - Sr * Sp).astype(f32)
             e = (a * np.abs(a)) * ivr
             e = e * ivp
-            c = np.where(ok, f32(1) - e, f32(2)).astype(f32)
-            mn = np.where(c < mn, c, mn)
-        vol[dl] = mn
+            best = np.where(ok & (e > best), e, best).astype(f32)
+        vol[dl] = f32(1) - best
     return vol
 
 

@@ -39,9 +39,17 @@
 namespace mvs {
 namespace {
 
+// Row-pair interleaved planes: element (y, x) of a view lives at uint2 index
+// ((y >> 1) * W + x) * 2 + (y & 1), over Hp = H rounded up to even rows, so
+// one 16-byte access returns rows 2m and 2m+1 of one column.
+__host__ __device__ __forceinline__ long pair_index(int y, int x, int W) {
+  return (((long)(y >> 1) * W + x) << 1) + (y & 1);
+}
+
 // ---- window statistics + packed intensities ------------------------------
-// one workgroup = 64 columns x 16 rows of one view; the (16+2R) x (64+2R)
-// byte tile is staged in LDS once.
+// one workgroup = 64 columns x 16 rows of one view; the (16+2R) x (64+8)
+// byte tile is staged in LDS once.  The dummy row H of an odd-height image
+// is written as an invalid window.
 constexpr int BS_TW = 64, BS_TH = 16;
 template <int R>
 __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q, int W, int H,
@@ -50,8 +58,9 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
   constexpr int TW = BS_TW + 8, TR = BS_TH + 2 * R;  // tile covers columns x0-R .. x0+63-R+7
   __shared__ uint8_t t[TR][TW + 4];
   const int x0 = blockIdx.x * BS_TW, y0 = blockIdx.y * BS_TH, z = blockIdx.z;
-  const long P = (long)W * H;
-  const uint8_t* Q = q + z * P;
+  const int Hp = H + (H & 1);
+  const long Pv = (long)W * Hp;  // plane elements per view
+  const uint8_t* Q = q + z * (long)W * H;
   for (int i = threadIdx.x; i < TR * TW; i += 256) {
     int r = i / TW, c = i % TW;
     int yy = y0 - R + r, xx = x0 - R + c;
@@ -64,7 +73,7 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int ly = ly0 + k, y = y0 + ly;
-    if (y >= H) break;
+    if (y >= Hp) break;
     int s = 0, ss = 0;
 #pragma unroll
     for (int j = 0; j < K; j++)
@@ -77,26 +86,32 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
     const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
     const int var = NK * ss - s * s;
     const float iv = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / (float)var : 0.0f);
-    const long o = z * P + (long)y * W + x;
+    const long o = z * Pv + pair_index(y, x, W);
     stats[o] = make_uint2((unsigned)(valid ? s : 0), (unsigned)__float_as_int(iv));
     const uint8_t* row = &t[ly + R][lx];
     unsigned lo = row[0] | (row[1] << 8) | (row[2] << 16) | ((unsigned)row[3] << 24);
     unsigned hi = row[4] | (row[5] << 8) | (row[6] << 16) | ((unsigned)row[7] << 24);
-    pk[o] = make_uint2(lo, hi);
+    pk[o] = y < H ? make_uint2(lo, hi) : make_uint2(0u, 0u);
   }
 }
 
 constexpr int kMaxNbr = 16;
 struct NccArgs {
   int W, H, D, nn, z;
+  int tiles_x, ntiles, tiles_per_xcd, nch;  // XCD-aware work map (see k_ncc_volume)
   int view[kMaxNbr];
-  int band_h, box_h;  // LDS band heights (rows); the row stride is the template BW
+  int pk_pairs, st_pairs;  // LDS band heights in row pairs; the pair-row stride is the template BW
 };
-// host-built plan (device memory, cached per context), passed as separate
-// __restrict__ kernel parameters so its loads are scalar (SMEM: they never
-// wait on the vector-memory counter that the LDS-DMA prefetch runs under):
-//   chunk[c][n] = {txmax, tymax, bh (pk rows to stage), sh (stats rows) | nblk << 16}
-//   lvl[n][dl]  = {txmax - tx, tymax - ty} of level dl in its chunk
+// host-built plan (device memory, cached per context): one 64-B record per
+// (chunk c, neighbour n, wave w), read with one scalar load per neighbour.
+// A __restrict__ kernel parameter, so the loads are SMEM and never wait on
+// the vector-memory counter the LDS-DMA prefetch runs under.
+struct alignas(64) NccRec {
+  int txmax, tymax;  // band origin: image column x0 - txmax; pk pair (y0-R-tymax)>>1, stats pair (y0-tymax)>>1
+  int bhp, shp;      // pk pair rows to stage, stats pair rows | (64-px blocks per row) << 16
+  int lv[8];         // per level j of wave w: {txmax - tx, pk start row | stats start row << 16 (band-relative)}
+  int pad[4];
+};
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gptr_t;
@@ -113,63 +128,129 @@ __device__ __forceinline__ float vmax(float acc, float e) {
   return r;
 }
 
-template <int K, int TH, int DPW, int BW>
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// N consecutive band rows starting at band row r0 of a row-pair band (pair
+// row stride BW, one column): ds_read_b128 per pair; an odd start takes the
+// first and last rows as ds_read_b64 halves.  N even.
+template <int N, int BW, bool EVEN>
+__device__ __forceinline__ void read_rows(const u32x4* col, int r0, u32x2 (&v)[N]) {
+  const u32x4* p = col + (r0 >> 1) * BW;
+  if (EVEN || (r0 & 1) == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 2; i++) {
+      const u32x4 t = p[i * BW];
+      v[2 * i] = t.xy;
+      v[2 * i + 1] = t.zw;
+    }
+  } else {
+    v[0] = ((const u32x2*)p)[1];
+#pragma unroll
+    for (int i = 1; i < N / 2; i++) {
+      const u32x4 t = p[i * BW];
+      v[2 * i - 1] = t.xy;
+      v[2 * i] = t.zw;
+    }
+    v[N - 1] = ((const u32x2*)(p + (N / 2) * BW))[0];
+  }
+}
+
+// EVEN: every level's band rows start on a pair boundary (all horizontal
+// neighbours with even R + tymax): branch-free pair reads.
+template <int K, int TH, int DPW, int BW, bool EVEN>
 __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ stats, const uint2* __restrict__ pk,
-                                                    const int4* __restrict__ plan_chunk,
-                                                    const int2* __restrict__ plan_lvl, NccArgs a,
+                                                    const NccRec* __restrict__ plan, NccArgs a,
                                                     float* __restrict__ vol) {
   constexpr int R = K / 2;
   constexpr int NR = TH + 2 * R;
   constexpr int NK = K * K;
   constexpr int DC = 4 * DPW;
+  static_assert(TH % 2 == 0 && NR % 2 == 0, "row pairs");
   // taps x-R .. x-R+3 in lo, x-R+4 .. x+R in the low K-4 bytes of hi
   constexpr unsigned HI_MASK = (K - 4) >= 4 ? 0xffffffffu : ((1u << (8 * (K - 4))) - 1u);
   extern __shared__ __align__(16) uint8_t smem[];
-  const int nbuf = (a.band_h + a.box_h) * BW;  // uint2 per neighbour buffer
-  uint2* nbase = (uint2*)smem;                 // 2 x {npk[band_h][BW], nst[box_h][BW]}
+  const int nbuf = (a.pk_pairs + a.st_pairs) * BW;  // uint4 per neighbour buffer
+  u32x4* nbase = (u32x4*)smem;                      // 2 x {npk[pk_pairs][BW], nst[st_pairs][BW]}
 
   // wave id made provably uniform: plan loads become scalar (SMEM), so no
   // vector-memory wait drains the in-flight LDS-DMA prefetch
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int W = a.W, H = a.H;
+  const int Hp2 = (H + 1) >> 1;  // row pairs per view
+  const long Pv = (long)W * Hp2 * 2;
   const long P = (long)W * H;
-  const int x0 = blockIdx.x * 64;
-  const int y0 = blockIdx.y * TH;
-  const int c = blockIdx.z;
-  const int d_lo = c * DC, d_hi = min(a.D, d_lo + DC);
+  // One workgroup per 64 x TH tile, looping over every level chunk c and
+  // neighbour n: a single pipeline of (c, n) steps whose neighbour bands are
+  // LDS-DMA double-buffered, so the reference rows are loaded once per tile
+  // and only the first band's latency is exposed.
+  // XCD-aware map: blocks are dealt round-robin over the 8 XCDs, so block b
+  // works in XCD-group b % 8; each group takes a contiguous strip of tiles,
+  // whose neighbour bands and halos then overlap in its L2.
+  const int bid = blockIdx.x, grp = bid & 7;
+  const int tile = grp * a.tiles_per_xcd + (bid >> 3);
+  if (tile >= a.ntiles) return;  // padding block (whole workgroup, before any barrier)
+  const int x0 = (tile % a.tiles_x) * 64;
+  const int y0 = (tile / a.tiles_x) * TH;  // even
   const int x = x0 + lane;
-  const int4* chunk = plan_chunk + c * a.nn;
+  const int nn = a.nn, T = a.nch * nn;   // pipeline steps
+  const NccRec* rec = plan + wave;       // record of step t = c*nn + n for this wave at rec[4 * t]
 
-  // LDS-DMA staging of neighbour n's bands into buffer b.  Band column j is
-  // image column x0 - txmax + j; band row r of pk is image row y0-R-tymax+r,
-  // of stats y0-tymax+r.  Columns and rows are clamped into the image: an
-  // edge pixel's window is invalid (NaN ivr) for R >= 1, so clamped cells
-  // never contribute.  A lane moves 2 px (16 B); pairs are clamped as a pair.
-  auto stage = [&](int n, int b) {
-    const int4 e = chunk[n];
-    const int bh = e.z, sh = e.w & 0xffff, nblk = e.w >> 16;
-    const int bx0 = x0 - e.x, by0 = y0 - R - e.y, sy0 = y0 - e.y;
-    const long vo = (long)a.view[n] * P;
-    uint2* npk = nbase + b * nbuf;
-    uint2* nst = npk + a.band_h * BW;
+  // LDS-DMA staging of step t's neighbour bands into buffer b.  Band column j
+  // is image column x0 - txmax + j; band pair row i of pk holds image rows
+  // 2(pm0+i), 2(pm0+i)+1 with pm0 = (y0-R-tymax)>>1 (stats: (y0-tymax)>>1).
+  // Columns and pairs are clamped into the image: edge pixels' windows are
+  // invalid (NaN ivr) for R >= 2, so clamped cells never contribute.
+  auto stage = [&](int t, int n, int b) {
+    const NccRec& e = rec[4 * t];
+    const int bhp = e.bhp, shp = e.shp & 0xffff, nblk = e.shp >> 16;
+    const int pm0 = (y0 - R - e.tymax) >> 1, sm0 = (y0 - e.tymax) >> 1;
+    const long vo = (long)a.view[n] * Pv;
+    u32x4* npk = nbase + b * nbuf;
+    u32x4* nst = npk + a.pk_pairs * BW;
     for (int cb = 0; cb < nblk; cb++) {
-      const uint2* gpk = pk + vo + min(max(bx0 + cb * 128 + 2 * lane, 0), W - 2);
-      const uint2* gst = stats + vo + min(max(bx0 + cb * 128 + 2 * lane, 0), W - 2);
-      for (int r = wave; r < bh; r += 4)
-        glds_b128(gpk + (long)min(max(by0 + r, 0), H - 1) * W, npk + r * BW + cb * 128);
-      for (int r = wave; r < sh; r += 4)
-        glds_b128(gst + (long)min(max(sy0 + r, 0), H - 1) * W, nst + r * BW + cb * 128);
+      const int xx = min(max(x0 - e.txmax + cb * 64 + lane, 0), W - 1);
+      const uint2* gpk = pk + vo + 2 * xx;
+      const uint2* gst = stats + vo + 2 * xx;
+      for (int i = wave; i < bhp; i += 4)
+        glds_b128(gpk + 2L * W * min(max(pm0 + i, 0), Hp2 - 1), npk + i * BW + cb * 64);
+      for (int i = wave; i < shp; i += 4)
+        glds_b128(gst + 2L * W * min(max(sm0 + i, 0), Hp2 - 1), nst + i * BW + cb * 64);
+    }
+  };
+  float E[DPW][TH];
+  auto reset = [&]() {
+#pragma unroll
+    for (int j = 0; j < DPW; j++)
+#pragma unroll
+      for (int o = 0; o < TH; o++) E[j][o] = -1.0f;
+  };
+  auto store = [&](int c) {  // cost = 1 - E of chunk c's levels; partial tiles/chunks masked
+    if (x >= W) return;
+#pragma unroll
+    for (int j = 0; j < DPW; j++) {
+      const int dl = c * DC + wave + 4 * j;
+      if (dl >= a.D) break;
+      float* vd = vol + (long)dl * P;
+#pragma unroll
+      for (int o = 0; o < TH; o++)
+        if (y0 + o < H) vd[(long)(y0 + o) * W + x] = 1.0f - E[j][o];
     }
   };
 
-  if (a.nn > 0) stage(0, 0);
+  reset();
+  if (T == 0) {  // no neighbours: every window invalid, cost 2
+    for (int c = 0; c < a.nch; c++) store(c);
+    return;
+  }
+  stage(0, 0, 0);
   // reference: packed rows y0-R .. y0+TH+R-1 and window stats of rows y0 .. y0+TH-1
-  const long zo = (long)a.z * P;
+  const long zo = (long)a.z * Pv;
   const int xc = min(x, W - 1);
   unsigned qlo[NR], qhi[NR];
 #pragma unroll
   for (int k = 0; k < NR; k++) {
-    const uint2 v = pk[zo + (long)min(max(y0 - R + k, 0), H - 1) * W + xc];
+    const uint2 v = pk[zo + pair_index(min(max(y0 - R + k, 0), H - 1), xc, W)];
     qlo[k] = v.x;
     qhi[k] = v.y & HI_MASK;
   }
@@ -177,120 +258,140 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
   float ivr[TH];
 #pragma unroll
   for (int o = 0; o < TH; o++) {
-    const uint2 v = stats[zo + (long)min(y0 + o, H - 1) * W + xc];
+    const uint2 v = stats[zo + pair_index(min(y0 + o, H - 1), xc, W)];
     nsr[o] = -(int)v.x;
     ivr[o] = __int_as_float((int)v.y);
   }
-  float E[DPW][TH];
-#pragma unroll
-  for (int j = 0; j < DPW; j++)
-#pragma unroll
-    for (int o = 0; o < TH; o++) E[j][o] = -1.0f;
   __syncthreads();
 
-  for (int n = 0; n < a.nn; n++) {
-    if (n + 1 < a.nn) stage(n + 1, (n + 1) & 1);  // prefetch while computing n
-    const uint2* npk = nbase + (n & 1) * nbuf;
-    const uint2* nst = npk + a.band_h * BW;
-    const int2* lv = plan_lvl + n * a.D;
+  int n = 0, c = 0;
+  for (int t = 0; t < T; t++) {
+    const int n1 = n + 1 == nn ? 0 : n + 1;
+    if (t + 1 < T) stage(t + 1, n1, (t + 1) & 1);  // prefetch step t+1 while computing t
+    const u32x4* npk = nbase + (t & 1) * nbuf;
+    const u32x4* nst = npk + a.pk_pairs * BW;
+    int lvv[2 * DPW];  // one scalar load of this wave's level shifts for step t
+#pragma unroll
+    for (int i = 0; i < 2 * DPW; i++) lvv[i] = rec[4 * t].lv[i];
+    // levels past the end of the last chunk carry in-band dummy shifts: they
+    // are computed and dropped at the store, so the loop is straight-line
 #pragma unroll
     for (int j = 0; j < DPW; j++) {
-      const int dl = d_lo + wave + 4 * j;
-      if (dl >= d_hi) break;  // wave-uniform
-      const int2 sh = lv[dl];  // {band column of x0 - tx, band row of y0 - R - ty}
-      const uint2* p = npk + sh.y * BW + sh.x + lane;
+      const int colo = lvv[2 * j], rows = lvv[2 * j + 1];
+      u32x2 pv[NR];
+      if (EVEN)
+        read_rows<NR, BW, true>(npk + colo + lane, rows & 0xffff, pv);
+      else
+        read_rows<NR, BW, false>(npk + colo + lane, rows & 0xffff, pv);
       int hs[NR];
 #pragma unroll
-      for (int k = 0; k < NR; k++) {
-        const uint2 v = p[k * BW];
-        hs[k] = (int)__builtin_amdgcn_udot4(qhi[k], v.y, __builtin_amdgcn_udot4(qlo[k], v.x, 0u, false), false);
-      }
-      const uint2* s = nst + sh.y * BW + sh.x + lane;
+      for (int k = 0; k < NR; k++)
+        hs[k] = (int)__builtin_amdgcn_udot4(qhi[k], pv[k].y, __builtin_amdgcn_udot4(qlo[k], pv[k].x, 0u, false),
+                                            false);
+      u32x2 sv[TH];
+      if (EVEN)
+        read_rows<TH, BW, true>(nst + colo + lane, rows >> 16, sv);
+      else
+        read_rows<TH, BW, false>(nst + colo + lane, rows >> 16, sv);
       int srp = 0;
 #pragma unroll
       for (int k = 0; k < 2 * R; k++) srp += hs[k];
 #pragma unroll
       for (int o = 0; o < TH; o++) {
         srp += hs[o + 2 * R];
-        const uint2 st = s[o * BW];
-        const int num = __mul24(NK, srp) + __mul24(nsr[o], (int)st.x);
+        const int num = __mul24(NK, srp) + __mul24(nsr[o], (int)sv[o].x);
         const float fa = (float)num;
         float e = fa * fabsf(fa);
         e = e * ivr[o];
-        e = e * __int_as_float((int)st.y);
+        e = e * __int_as_float((int)sv[o].y);
         E[j][o] = vmax(E[j][o], e);
         srp -= hs[o];
       }
     }
-    __syncthreads();  // next bands landed (vmcnt 0); this buffer free for n+2
-  }
-  if (x >= W) return;
-#pragma unroll
-  for (int j = 0; j < DPW; j++) {
-    const int dl = d_lo + wave + 4 * j;
-    if (dl >= d_hi) break;
-    float* vd = vol + (long)dl * P;
-#pragma unroll
-    for (int o = 0; o < TH; o++)
-      if (y0 + o < H) vd[(long)(y0 + o) * W + x] = 1.0f - E[j][o];
+    if (n1 == 0) {  // chunk c complete
+      store(c);
+      reset();
+      c++;
+    }
+    n = n1;
+    __syncthreads();  // step t+1's bands landed (vmcnt 0); this buffer free for t+2
   }
 }
 
 // Host side: the chunk/level shift plan (every roundf of the definition is
 // evaluated here, once per distinct configuration) and the launch.
 struct NccPlan {
-  std::vector<int32_t> table;  // chunk int4 [nchunks][nn], then lvl int2 [nn][D]
-  int band_w = 0, band_h = 0, box_h = 0;
+  std::vector<int32_t> table;  // NccRec [nchunks][nn][4 waves] as int32
+  int band_w = 0, pk_pairs = 0, st_pairs = 0;
+  bool even = true;  // every level's band rows start on a pair boundary
 };
+
+inline int floor_half(int v) { return v >> 1; }  // arithmetic: floor(v / 2)
 
 template <int K, int TH, int DPW>
 NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl) {
   constexpr int R = K / 2, NR = TH + 2 * R, DC = 4 * DPW;
+  static_assert(DPW <= 4, "NccRec holds 4 levels per wave");
+  constexpr int RW = sizeof(NccRec) / 4;
   const int nch = (D + DC - 1) / DC;
   NccPlan p;
-  p.table.assign((size_t)nch * nn * 4 + (size_t)nn * D * 2, 0);
-  int32_t* ch = p.table.data();
-  int32_t* lv = ch + (size_t)nch * nn * 4;
-  int spx = 0, spy = 0;
+  p.table.assign((size_t)nch * nn * 4 * RW, 0);
+  int spx = 0;
+  auto tx_of = [&](int dl, int n) { return (int)roundf(levels[dl] * fdx[n]); };
+  auto ty_of = [&](int dl, int n) { return (int)roundf((bl * levels[dl]) * fdy[n]); };
+  // y0 is even (TH even), so every row parity below is independent of y0
   for (int c = 0; c < nch; c++)
     for (int n = 0; n < nn; n++) {
       int txmin = 1 << 30, txmax = -(1 << 30), tymin = 1 << 30, tymax = -(1 << 30);
       for (int dl = c * DC; dl < std::min(D, c * DC + DC); dl++) {
-        const float d = levels[dl];
-        const int tx = (int)roundf(d * fdx[n]), ty = (int)roundf((bl * d) * fdy[n]);
-        txmin = std::min(txmin, tx); txmax = std::max(txmax, tx);
-        tymin = std::min(tymin, ty); tymax = std::max(tymax, ty);
+        txmin = std::min(txmin, tx_of(dl, n)); txmax = std::max(txmax, tx_of(dl, n));
+        tymin = std::min(tymin, ty_of(dl, n)); tymax = std::max(tymax, ty_of(dl, n));
       }
-      for (int dl = c * DC; dl < std::min(D, c * DC + DC); dl++) {
-        const float d = levels[dl];
-        const int tx = (int)roundf(d * fdx[n]), ty = (int)roundf((bl * d) * fdy[n]);
-        lv[2 * ((size_t)n * D + dl)] = txmax - tx;
-        lv[2 * ((size_t)n * D + dl) + 1] = tymax - ty;
+      const int pb = -R - tymax, sb = -tymax;            // band first image row - y0
+      const int pr = pb - 2 * floor_half(pb), sr = sb - 2 * floor_half(sb);  // its parity in the pair band
+      const int bhp = (pr + NR + tymax - tymin + 1) >> 1;  // pairs covering every level's rows
+      const int shp = (sr + TH + tymax - tymin + 1) >> 1;
+      const int nblk = (64 + txmax - txmin + 63) >> 6;
+      for (int w = 0; w < 4; w++) {
+        int32_t* e = p.table.data() + (((size_t)c * nn + n) * 4 + w) * RW;
+        e[0] = txmax;
+        e[1] = tymax;
+        e[2] = bhp;
+        e[3] = shp | (nblk << 16);
+        for (int j = 0; j < DPW; j++) {
+          const int dl = c * DC + w + 4 * j;
+          if (dl >= D) {  // dummy level past the end: the band origin's even rows
+            e[4 + 2 * j] = 0;
+            e[5 + 2 * j] = pr | (sr << 16);
+            continue;
+          }
+          const int ty = ty_of(dl, n);
+          e[4 + 2 * j] = txmax - tx_of(dl, n);
+          e[5 + 2 * j] = (pr + tymax - ty) | ((sr + tymax - ty) << 16);
+          if (((pr + tymax - ty) | (sr + tymax - ty)) & 1) p.even = false;
+        }
       }
-      const int nblk = (64 + txmax - txmin + 127) >> 7;
-      int32_t* e = ch + 4 * ((size_t)c * nn + n);
-      e[0] = txmax;
-      e[1] = tymax;
-      e[2] = NR + tymax - tymin;
-      e[3] = (TH + tymax - tymin) | (nblk << 16);
       spx = std::max(spx, txmax - txmin);
-      spy = std::max(spy, tymax - tymin);
+      p.pk_pairs = std::max(p.pk_pairs, bhp);
+      p.st_pairs = std::max(p.st_pairs, shp);
     }
-  p.band_w = (64 + spx + 127) & ~127;  // whole 128-px LDS-DMA pieces per row
-  p.band_h = NR + spy;
-  p.box_h = TH + spy;
+  p.band_w = (64 + spx + 63) & ~63;  // whole 64-column LDS-DMA pieces per pair row
   return p;
 }
 
-template <int K, int TH, int DPW, int BW>
-int launch_ncc_bw(hipStream_t s, const uint2* stats, const uint2* pk, const int4* chunk, const int2* lvl,
-                  NccArgs& a, float* vol, size_t lds) {
+template <int K, int TH, int DPW, int BW, bool EVEN>
+int launch_ncc_bw(hipStream_t s, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
+                  size_t lds) {
   constexpr int DC = 4 * DPW;
-  dim3 g((a.W + 63) / 64, (a.H + TH - 1) / TH, (a.D + DC - 1) / DC);
+  a.tiles_x = (a.W + 63) / 64;
+  a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);
+  a.tiles_per_xcd = (a.ntiles + 7) / 8;
+  a.nch = (a.D + DC - 1) / DC;
+  dim3 g(8 * a.tiles_per_xcd);
   if (lds > 64 * 1024)
-    MVS_HIP(hipFuncSetAttribute((const void*)k_ncc_volume<K, TH, DPW, BW>,
+    MVS_HIP(hipFuncSetAttribute((const void*)k_ncc_volume<K, TH, DPW, BW, EVEN>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute(ncc lds)");
-  hipLaunchKernelGGL((k_ncc_volume<K, TH, DPW, BW>), g, dim3(256), lds, s, stats, pk, chunk, lvl, a, vol);
+  hipLaunchKernelGGL((k_ncc_volume<K, TH, DPW, BW, EVEN>), g, dim3(256), lds, s, stats, pk, plan, a, vol);
   MVS_LAUNCH_CHECK("k_ncc_volume");
   return 0;
 }
@@ -300,26 +401,31 @@ template <int K, int TH, int DPW>
 int launch_ncc_t(mvs_ctx* ctx, const uint2* stats, const uint2* pk, NccArgs& a, const float* levels_host,
                  const float* fdx, const float* fdy, float bl, float* vol) {
   NccPlan p = make_plan<K, TH, DPW>(levels_host, a.D, a.nn, fdx, fdy, bl);
-  const size_t lds = 2 * 8 * (size_t)(p.band_h + p.box_h) * p.band_w;
-  if (lds > 160 * 1024 || (p.band_w != 128 && p.band_w != 256)) return 1;
+  const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * p.band_w;
+  if (lds > 160 * 1024 || p.band_w > 256) return 1;
   int rc = 0;
   const int32_t* dev = plan_upload(ctx, p.table, &rc);
   if (rc) return rc;
-  a.band_h = p.band_h;
-  a.box_h = p.box_h;
-  const int nch = (a.D + 4 * DPW - 1) / (4 * DPW);
-  const int4* chunk = (const int4*)dev;
-  const int2* lvl = (const int2*)(dev + (size_t)nch * a.nn * 4);
-  if (p.band_w == 128) return launch_ncc_bw<K, TH, DPW, 128>(ctx->stream, stats, pk, chunk, lvl, a, vol, lds);
-  return launch_ncc_bw<K, TH, DPW, 256>(ctx->stream, stats, pk, chunk, lvl, a, vol, lds);
+  a.pk_pairs = p.pk_pairs;
+  a.st_pairs = p.st_pairs;
+  const NccRec* plan = (const NccRec*)dev;
+  if (p.even) {
+    if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, 128, true>(ctx->stream, stats, pk, plan, a, vol, lds);
+    if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, 192, true>(ctx->stream, stats, pk, plan, a, vol, lds);
+    return launch_ncc_bw<K, TH, DPW, 256, true>(ctx->stream, stats, pk, plan, a, vol, lds);
+  }
+  if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, 128, false>(ctx->stream, stats, pk, plan, a, vol, lds);
+  if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, 192, false>(ctx->stream, stats, pk, plan, a, vol, lds);
+  return launch_ncc_bw<K, TH, DPW, 256, false>(ctx->stream, stats, pk, plan, a, vol, lds);
 }
 
 }  // namespace
 
 int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box) {
+  const int Hp = H + (H & 1);
   uint2* stats = (uint2*)box;
-  uint2* pk = stats + (long)V * W * H;
-  dim3 g((W + BS_TW - 1) / BS_TW, (H + BS_TH - 1) / BS_TH, V);
+  uint2* pk = stats + (long)V * W * Hp;
+  dim3 g((W + BS_TW - 1) / BS_TW, (Hp + BS_TH - 1) / BS_TH, V);
   if (K == 5)
     hipLaunchKernelGGL(k_box_stats<2>, g, dim3(256), 0, s, l8, W, H, stats, pk);
   else
@@ -345,7 +451,7 @@ int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, con
     fdy[n] = (float)(v / aw - ry);
   }
   const uint2* stats = (const uint2*)box;
-  const uint2* pk = stats + (long)V * W * H;
+  const uint2* pk = stats + (long)V * W * (H + (H & 1));
   // tile height and levels per wave: MVS_NCC_TH (8|16), MVS_NCC_DPW (1|2|4)
   static const int dpw_env = [] {
     const char* e = getenv("MVS_NCC_DPW");

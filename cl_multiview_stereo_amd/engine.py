@@ -156,8 +156,9 @@ class Engine:
 
     def box_stats(self, l8, K: int = 5, out=None):
         V, H, W = l8.shape
-        # [0] window stats {S, bits(1/var | NaN)}, [1] packed intensities {lo, hi}
-        out = self.empty((2, V, H, W, 2), torch.int32) if out is None else out
+        # [0] window stats {S, bits(1/var | NaN)}, [1] packed intensities {lo, hi};
+        # rows pairwise interleaved over Hp = H rounded up to even (include/mvs.h)
+        out = self.empty((2, V, H + (H & 1), W, 2), torch.int32) if out is None else out
         self._stream()
         _lib.check(self.L.mvs_box_stats_d(self.ctx, _ptr(l8), V, W, H, K, _ptr(out)), "mvs_box_stats_d")
         return out

@@ -116,9 +116,11 @@ int mvs_sweep_pixel_sad_d(mvs_ctx* ctx, int W, int H, const float* lab, const mv
                           float* disp);
 
 /* Build-defined per-pixel NCC KxK plane sweep (definition: csrc/ncc.hip).
- * box int32 [2][V][H][W][2] (16 B/px, from mvs_box_stats_d): plane 0 per-pixel
- * window statistics {S = sum q, bits(1/(n*sum q^2 - S^2)) (0 if textureless,
- * NaN if the window leaves the image)}; plane 1 the packed intensities
+ * box int32 [2][V][Hp][W][2] (Hp = H rounded up to even; 16 B/px), from
+ * mvs_box_stats_d, rows stored pairwise interleaved (element (y, x) of a view
+ * at uint2 index ((y>>1)*W + x)*2 + (y&1)): plane 0 per-pixel window
+ * statistics {S = sum q, bits(1/(n*sum q^2 - S^2)) (0 if textureless, NaN if
+ * the window leaves the image)}; plane 1 the packed intensities
  * q(x-R .. x-R+7) of each pixel's row (two little-endian dwords).
  * vol [D][H][W] float cost of reference view z = 1 - max(-1, best signed
  * squared NCC over valid neighbour windows); l8 is validated only. */

@@ -1,6 +1,7 @@
 // C-ABI of libmvs.so (include/mvs.h): context management, argument checking,
 // metadata upload and the stage orchestration that the reference's host stage
 // classes perform (clSLIC, clPhotoConsistency, clDepthRefinement).
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -217,16 +218,21 @@ int mvs_slic_d(mvs_ctx* c, const float* lab, int V, int W, int H, const mvs_slic
   xy = xy * xy;
   col = col * col;
   hipStream_t s = c->stream;
+  // one scratch for the update partials and the connectivity pass
+  size_t sb = std::max(mvs::update_scratch_bytes(V, W, H, S),
+                       p->enforce_connectivity ? sizeof(uint32_t) * (size_t)V * W * H : (size_t)0);
+  int rc = 0;
+  void* scr = sb ? mvs::scratch(c, sb, &rc) : nullptr;
+  if (rc) return rc;
+  float* part = mvs::update_scratch_bytes(V, W, H, S) ? (float*)scr : nullptr;
   RC(mvs::launch_init_centers(s, lab, V, W, H, S, spixl));
   RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
   for (int i = 0; i < p->no_iter; i++) {
-    RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl));
+    RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl, part));
     RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
   }
   if (p->enforce_connectivity) {
-    int rc = 0;
-    uint32_t* tmp = (uint32_t*)mvs::scratch(c, sizeof(uint32_t) * (size_t)V * W * H, &rc);
-    if (rc) return rc;
+    uint32_t* tmp = (uint32_t*)scr;
     RC(mvs::launch_suppress(s, labels, tmp, V, W, H));
     RC(mvs::launch_suppress(s, tmp, labels, V, W, H));
   }

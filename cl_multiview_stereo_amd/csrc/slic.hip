@@ -199,6 +199,97 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
   }
 }
 
+// ---- the same update when S is a multiple of 16 --------------------------
+// Every superpixel window then starts on the global 16x16 tile grid, so each
+// image tile is tile t = nby*cpl + nbx of exactly the 3x3 superpixels whose
+// windows cover it.  One wave per image tile reads its 256 pixels ONCE (the
+// per-superpixel kernel above reads each pixel 9 times) and reduces, for each
+// of those superpixels, its members with the reference's LDS tree order
+// (wave_tree); non-members and other superpixels contribute exact zeros.
+// k_update_finalize then sums each superpixel's G partials in tile order --
+// bit-identical to k_update.
+__global__ __launch_bounds__(256) void k_update_tiles(const float4* __restrict__ lab,
+                                                      const uint32_t* __restrict__ labels, int W, int H, int S,
+                                                      int mw, int mh, int G, int cpl, int ntx, int nty,
+                                                      float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x * 4 + wave, z = blockIdx.y;
+  if (tile >= ntx * nty) return;  // no barriers below
+  const int TX = tile % ntx, TY = tile / ntx, s16 = S / 16;
+  const long P = (long)W * H;
+  const float4* L = lab + (long)z * P;
+  const uint32_t* I = labels + (long)z * P;
+  const int lx = lane & 15, ly0 = lane >> 4;  // local index k = lane + 64*m, as the reference tile
+  uint32_t lbl[4];
+  float4 c[4];
+  float fx[4], fy[4];
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int px = TX * 16 + lx, py = TY * 16 + ly0 + 4 * m;
+    const bool in = px < W && py < H;
+    lbl[m] = in ? I[(long)py * W + px] : 0xffffffffu;
+    c[m] = in ? L[(long)py * W + px] : make_float4(0.f, 0.f, 0.f, 0.f);
+    fx[m] = (float)px;
+    fy[m] = (float)py;
+  }
+  float* out = part + (long)z * mw * mh * G * 6;
+  for (int gy = TY / s16 - 1; gy <= TY / s16 + 1; gy++) {
+    if (gy < 0 || gy >= mh) continue;
+    for (int gx = TX / s16 - 1; gx <= TX / s16 + 1; gx++) {
+      if (gx < 0 || gx >= mw) continue;
+      const uint32_t sp = (uint32_t)(gy * mw + gx);
+      const int t = (TY - (gy - 1) * s16) * cpl + (TX - (gx - 1) * s16);
+      bool mem[4], any = false;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        mem[m] = lbl[m] == sp;
+        any |= mem[m];
+      }
+      float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (__any(any)) {
+        r[0] = wave_tree(mem[0] ? fx[0] : 0.f, mem[1] ? fx[1] : 0.f, mem[2] ? fx[2] : 0.f, mem[3] ? fx[3] : 0.f);
+        r[1] = wave_tree(mem[0] ? fy[0] : 0.f, mem[1] ? fy[1] : 0.f, mem[2] ? fy[2] : 0.f, mem[3] ? fy[3] : 0.f);
+        r[2] = wave_tree(mem[0] ? c[0].x : 0.f, mem[1] ? c[1].x : 0.f, mem[2] ? c[2].x : 0.f, mem[3] ? c[3].x : 0.f);
+        r[3] = wave_tree(mem[0] ? c[0].y : 0.f, mem[1] ? c[1].y : 0.f, mem[2] ? c[2].y : 0.f, mem[3] ? c[3].y : 0.f);
+        r[4] = wave_tree(mem[0] ? c[0].z : 0.f, mem[1] ? c[1].z : 0.f, mem[2] ? c[2].z : 0.f, mem[3] ? c[3].z : 0.f);
+        r[5] = wave_tree(mem[0] ? 1.f : 0.f, mem[1] ? 1.f : 0.f, mem[2] ? 1.f : 0.f, mem[3] ? 1.f : 0.f);
+      }
+      if (lane == 0) {  // the tree's result lives in lane 0
+#pragma unroll
+        for (int ch = 0; ch < 6; ch++) out[((long)sp * G + t) * 6 + ch] = r[ch];
+      }
+    }
+  }
+}
+
+__global__ void k_update_finalize(const float* __restrict__ part, int mw, int mh, int S, int G, int cpl, int ntx,
+                                  int nty, float* __restrict__ spixl) {
+  const int sp = blockIdx.x * blockDim.x + threadIdx.x, z = blockIdx.y;
+  if (sp >= mw * mh) return;
+  const int gx = sp % mw, gy = sp / mw, s16 = S / 16;
+  const float* pp = part + ((long)z * mw * mh + sp) * G * 6;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < G; t++) {
+    const int TX = (gx - 1) * s16 + t % cpl, TY = (gy - 1) * s16 + t / cpl;
+    if (TX < 0 || TY < 0 || TX >= ntx || TY >= nty) continue;  // outside the image: the reference adds 0
+#pragma unroll
+    for (int ch = 0; ch < 6; ch++) acc[ch] = acc[ch] + pp[t * 6 + ch];
+  }
+  float* o = spixl + 8 * ((long)z * mw * mh + sp);
+  const float n = acc[5];
+  o[0] = (float)sp;
+  if (n != 0) {
+    o[1] = acc[0] / n;
+    o[2] = acc[1] / n;
+    o[3] = acc[2] / n;
+    o[4] = acc[3] / n;
+    o[5] = acc[4] / n;
+    o[6] = n;
+  } else {
+    o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
+  }
+}
+
 // ---- supress_local_lable, clcode.cl:676-711 ------------------------------
 __global__ void k_suppress(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, int W, int H) {
   int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
@@ -257,12 +348,29 @@ int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, in
   return 0;
 }
 
+size_t update_scratch_bytes(int V, int W, int H, int S) {
+  if (S % 16 != 0) return 0;
+  int mw = map_dim(W, S), mh = map_dim(H, S);
+  int G = (3 * S / kLocal) * (3 * S / kLocal);
+  return sizeof(float) * 6 * (size_t)G * mw * mh * V;
+}
+
 int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V, int W, int H, int S,
-                  float* spixl) {
+                  float* spixl, float* part) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
   int G = (int)__builtin_ceilf((float)(S * S * 9) / (float)(kLocal * kLocal));
   int cpl = S * 3 / kLocal;
   if (cpl <= 0) return arg_fail("SLIC update needs spixl_size >= 6 (cluster_per_line = 3S/16 > 0)");
+  if (part && S % 16 == 0) {  // tile-grid path (each pixel read once)
+    int ntx = (W + 15) / 16, nty = (H + 15) / 16;
+    hipLaunchKernelGGL(k_update_tiles, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, labels,
+                       W, H, S, mw, mh, G, cpl, ntx, nty, part);
+    MVS_LAUNCH_CHECK("k_update_tiles");
+    hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 63) / 64, V), dim3(64), 0, s, part, mw, mh, S, G, cpl,
+                       ntx, nty, spixl);
+    MVS_LAUNCH_CHECK("k_update_finalize");
+    return 0;
+  }
   size_t lds = sizeof(float) * 6 * (size_t)G;
   if (lds > 64 * 1024) return arg_fail("spixl_size too large for the update kernel");
   hipLaunchKernelGGL(k_update, dim3(mw * mh, V), dim3(256), lds, s, (const float4*)lab, labels, W, H, S, mw, mh, G,

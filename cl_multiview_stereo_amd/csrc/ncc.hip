@@ -87,7 +87,10 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
     const int var = NK * ss - s * s;
     const float iv = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / (float)var : 0.0f);
     const long o = z * Pv + pair_index(y, x, W);
-    stats[o] = make_uint2((unsigned)(valid ? s : 0), (unsigned)__float_as_int(iv));
+    // window sum: K = 5 stores it centred, as a float (S - 128*n, exact), for
+    // the FP32 finish of k_ncc_volume; K = 7 stores the integer S
+    const unsigned sw = R == 2 ? (unsigned)__float_as_int((float)((valid ? s : 0) - 128 * NK)) : (unsigned)(valid ? s : 0);
+    stats[o] = make_uint2(sw, (unsigned)__float_as_int(iv));
     const uint8_t* row = &t[ly + R][lx];
     unsigned lo = row[0] | (row[1] << 8) | (row[2] << 16) | ((unsigned)row[3] << 24);
     unsigned hi = row[4] | (row[5] << 8) | (row[6] << 16) | ((unsigned)row[7] << 24);
@@ -167,6 +170,7 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
   constexpr int NK = K * K;
   constexpr int DC = 4 * DPW;
   static_assert(TH % 2 == 0 && NR % 2 == 0, "row pairs");
+  constexpr bool FPF = K == 5;  // FP32 finish (see the reference loads below)
   // taps x-R .. x-R+3 in lo, x-R+4 .. x+R in the low K-4 bytes of hi
   constexpr unsigned HI_MASK = (K - 4) >= 4 ? 0xffffffffu : ((1u << (8 * (K - 4))) - 1u);
   extern __shared__ __align__(16) uint8_t smem[];
@@ -231,10 +235,11 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
     for (int j = 0; j < DPW; j++) {
       const int dl = c * DC + wave + 4 * j;
       if (dl >= a.D) break;
-      float* vd = vol + (long)dl * P;
+      float* vd = vol + (long)dl * P;  // scalar base; 32-bit per-lane offsets (saddr stores)
+      const int off0 = y0 * W + x;
 #pragma unroll
       for (int o = 0; o < TH; o++)
-        if (y0 + o < H) vd[(long)(y0 + o) * W + x] = 1.0f - E[j][o];
+        if (y0 + o < H) vd[off0 + o * W] = 1.0f - E[j][o];
     }
   };
 
@@ -254,12 +259,25 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
     qlo[k] = v.x;
     qhi[k] = v.y & HI_MASK;
   }
-  int nsr[TH];  // -Sr, so num = n*Srp + (-Sr)*Sp is one mul24 + one mad24
+  // K = 5 (FPF): num = n*Srp - Sr*Sp evaluated in FP32 on centred sums
+  //   (Srp_c = Srp - 128(Sr + Sp) + 128^2 n, |n Srp_c|, |Sr_c Sp_c| <= 10.24M),
+  //   every intermediate an integer below 2^24 and one rounding at the final
+  //   fma: bit-identical to (float)num, at the FP32 issue rate (integer VALU
+  //   ops issue at half rate on gfx950).  K = 7 exceeds 2^24: integer finish.
+  // rs[o]: FPF -(Sr_c) as float, else -Sr as int bits;  ar[o]: -128 Sr_c - 128^2 n.
+  float rs[TH], ar[TH];
   float ivr[TH];
 #pragma unroll
   for (int o = 0; o < TH; o++) {
     const uint2 v = stats[zo + pair_index(min(y0 + o, H - 1), xc, W)];
-    nsr[o] = -(int)v.x;
+    if (FPF) {
+      const float src = __int_as_float((int)v.x);
+      rs[o] = -src;
+      ar[o] = -128.0f * src - (float)(128 * 128 * NK);
+    } else {
+      rs[o] = __int_as_float(-(int)v.x);
+      ar[o] = 0.0f;
+    }
     ivr[o] = __int_as_float((int)v.y);
   }
   __syncthreads();
@@ -283,29 +301,41 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
         read_rows<NR, BW, true>(npk + colo + lane, rows & 0xffff, pv);
       else
         read_rows<NR, BW, false>(npk + colo + lane, rows & 0xffff, pv);
-      int hs[NR];
+      // prefix sums over band rows of the horizontal K-tap correlation: the
+      // dot4 accumulator input carries the running sum (exact integers)
+      int ps[NR];
+      unsigned acc = 0u;
 #pragma unroll
-      for (int k = 0; k < NR; k++)
-        hs[k] = (int)__builtin_amdgcn_udot4(qhi[k], pv[k].y, __builtin_amdgcn_udot4(qlo[k], pv[k].x, 0u, false),
-                                            false);
+      for (int k = 0; k < NR; k++) {
+        acc = __builtin_amdgcn_udot4(qhi[k], pv[k].y, __builtin_amdgcn_udot4(qlo[k], pv[k].x, acc, false), false);
+        ps[k] = (int)acc;
+      }
       u32x2 sv[TH];
       if (EVEN)
         read_rows<TH, BW, true>(nst + colo + lane, rows >> 16, sv);
       else
         read_rows<TH, BW, false>(nst + colo + lane, rows >> 16, sv);
-      int srp = 0;
+      float pf[NR];
+      if (FPF) {
 #pragma unroll
-      for (int k = 0; k < 2 * R; k++) srp += hs[k];
+        for (int k = 0; k < NR; k++) pf[k] = (float)ps[k];  // < 2^24: exact
+      }
 #pragma unroll
       for (int o = 0; o < TH; o++) {
-        srp += hs[o + 2 * R];
-        const int num = __mul24(NK, srp) + __mul24(nsr[o], (int)sv[o].x);
-        const float fa = (float)num;
+        float fa;
+        if (FPF) {
+          const float spc = __int_as_float((int)sv[o].x);
+          const float srp = o > 0 ? pf[o + 2 * R] - pf[o - 1] : pf[2 * R];  // Srp, exact
+          const float src = __builtin_fmaf(-128.0f, spc, srp + ar[o]);     // Srp_c, exact
+          fa = __builtin_fmaf(rs[o], spc, (float)NK * src);                 // (float)num
+        } else {
+          const int srp = o > 0 ? ps[o + 2 * R] - ps[o - 1] : ps[2 * R];
+          fa = (float)(__mul24(NK, srp) + __mul24(__float_as_int(rs[o]), (int)sv[o].x));
+        }
         float e = fa * fabsf(fa);
         e = e * ivr[o];
         e = e * __int_as_float((int)sv[o].y);
         E[j][o] = vmax(E[j][o], e);
-        srp -= hs[o];
       }
     }
     if (n1 == 0) {  // chunk c complete

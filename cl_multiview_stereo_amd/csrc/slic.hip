@@ -76,44 +76,93 @@ __global__ void k_grid_labels(int W, int H, int S, int mw, uint32_t* __restrict_
 }
 
 // ---- slic_distance_function + find_center_association, clcode.cl:422-520 -
-__device__ __forceinline__ float slic_dist(float4 px, int y, int x, const float* c, float weight, float sn,
-                                           float cn) {
-  float a = (px.x - c[3]) * (px.x - c[3]);
-  a = a + (px.y - c[4]) * (px.y - c[4]);
-  a = a + (px.z - c[5]) * (px.z - c[5]);
-  float b = ((float)x - c[1]) * ((float)x - c[1]);
-  b = b + ((float)y - c[2]) * ((float)y - c[2]);
-  float d = (a * cn) + weight * (b * sn);
-  return sqrtf(d);
+// the argument of the reference's sqrt; the distance is sqrtf(slic_dist2)
+__device__ __forceinline__ float slic_dist2(float4 px, int y, int x, float4 c, float cb, float weight, float sn,
+                                            float cn) {
+  // c = (cx, cy, L, a), cb = b of the centre (spixl fields 1..5)
+  float a = (px.x - c.z) * (px.x - c.z);
+  a = a + (px.y - c.w) * (px.y - c.w);
+  a = a + (px.z - cb) * (px.z - cb);
+  float b = ((float)x - c.x) * ((float)x - c.x);
+  b = b + ((float)y - c.y) * ((float)y - c.y);
+  return (a * cn) + weight * (b * sn);
 }
 
+// A workgroup assigns a 64 x 16 pixel block; the centres of every cell that
+// can be a candidate of its pixels (one cell around the block's cells) are
+// staged in LDS once, so the per-pixel candidate reads are LDS broadcasts.
+constexpr int AS_TW = 64, AS_TH = 16, AS_MAXC = 128;
 __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, const float* __restrict__ spixl,
                                                 int W, int H, int S, int mw, int mh, float xy_n, float col_n,
                                                 float weight, uint32_t* __restrict__ labels) {
-  int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  int row = blockIdx.y * 4 + (threadIdx.x >> 6);
-  int z = blockIdx.z;
-  if (col >= W || row >= H) return;
-  long P = (long)W * H;
-  long pid = (long)z * P + (long)row * W + col;
+  __shared__ float4 cxyla[AS_MAXC];  // (cx, cy, L, a)
+  __shared__ float cbb[AS_MAXC];     // b
+  const int x0 = blockIdx.x * AS_TW, y0 = blockIdx.y * AS_TH, z = blockIdx.z;
+  const int cx0 = x0 / S - 1, cy0 = y0 / S - 1;
+  const int ncx = min(x0 + AS_TW - 1, W - 1) / S - x0 / S + 3;
+  const int ncy = min(y0 + AS_TH - 1, H - 1) / S - y0 / S + 3;
   const float* sp = spixl + 8L * z * mw * mh;
-  float4 px = lab[pid];
-  int cxg = col / S, cyg = row / S;
-  int dX = (col + S / 2) / S - cxg, dY = (row + S / 2) / S - cyg;
-  float min_dist = 999999.9999f, min_id = -1.0f;
-  for (int i = -1 + dX; i <= dX; i++)      // i spans the x delta but offsets y
-    for (int j = -1 + dY; j <= dY; j++) {  // (Appendix A #2, reproduced)
-      int cx = cxg + j, cy = cyg + i;
-      if (cx >= 0 && cy >= 0 && cx < mw && cy < mh) {
-        int ci = cy * mw + cx;
-        float d = slic_dist(px, row, col, sp + 8 * ci, weight, xy_n, col_n);
-        if (d < min_dist) {
-          min_dist = d;
-          min_id = (float)ci;
-        }
-      }
+  const int col = x0 + (threadIdx.x & 63);
+  const long P = (long)W * H;
+  constexpr int NRW = AS_TH / 4;
+  float4 pxs[NRW];  // the thread's pixels, loaded before the centre staging
+#pragma unroll
+  for (int r = 0; r < NRW; r++) {
+    const int row = min(y0 + (threadIdx.x >> 6) + 4 * r, H - 1);
+    pxs[r] = lab[(long)z * P + (long)row * W + min(col, W - 1)];
+  }
+  for (int e = threadIdx.x; e < ncx * ncy; e += 256) {
+    const int cx = cx0 + e % ncx, cy = cy0 + e / ncx;
+    if (cx >= 0 && cy >= 0 && cx < mw && cy < mh) {
+      const float* c = sp + 8 * (cy * mw + cx);
+      cxyla[e] = make_float4(c[1], c[2], c[3], c[4]);
+      cbb[e] = c[5];
     }
-  labels[pid] = (uint32_t)min_id;
+  }
+  __syncthreads();
+  if (col >= W) return;
+  // n / S as a multiply-high with M = ceil(2^32 / S): exact for n < 2^16, S <= 96
+  const unsigned M = 0xffffffffu / (unsigned)S + 1u;
+  auto divS = [&](int n) { return (int)__umulhi((unsigned)n, M); };
+  const int cxg = divS(col), dX = divS(col + S / 2) - cxg;
+#pragma unroll
+  for (int r = 0; r < NRW; r++) {
+    const int row = y0 + (threadIdx.x >> 6) + 4 * r;
+    if (row >= H) break;
+    const long pid = (long)z * P + (long)row * W + col;
+    const float4 px = pxs[r];
+    const int cyg = divS(row), dY = divS(row + S / 2) - cyg;
+    // The reference keeps the smallest sqrt(d2) (strict <, first in loop
+    // order).  sqrt is monotone, so a candidate with d2 >= the best d2 never
+    // wins, and one below it by more than 2^-20 relative always does; only a
+    // near tie needs the two correctly rounded square roots compared.
+    float best2 = 0.0f, min_id = -1.0f;
+    bool have = false;
+#pragma unroll
+    for (int ii = 0; ii < 2; ii++)
+#pragma unroll
+      for (int jj = 0; jj < 2; jj++) {  // i spans the x delta but offsets y (Appendix A #2)
+        const int cx = cxg + (jj - 1 + dY), cy = cyg + (ii - 1 + dX);
+        const bool ok = cx >= 0 && cy >= 0 && cx < mw && cy < mh;
+        const int e = ok ? (cy - cy0) * ncx + (cx - cx0) : 0;
+        const float d2 = slic_dist2(px, row, col, cxyla[e], cbb[e], weight, xy_n, col_n);
+        bool take;
+        if (!have) {
+          take = d2 < 9.0e11f || sqrtf(d2) < 999999.9999f;  // the reference's initial min_dist
+        } else if (d2 >= best2) {
+          take = false;
+        } else if (d2 < best2 * 0.99999905f) {
+          take = true;
+        } else {
+          take = sqrtf(d2) < sqrtf(best2);
+        }
+        take = take && ok;
+        best2 = take ? d2 : best2;
+        min_id = take ? (float)(cy * mw + cx) : min_id;
+        have = have || take;
+      }
+    labels[pid] = (uint32_t)min_id;
+  }
 }
 
 // ---- update_cluster_center + finalize_reduction_result -------------------
@@ -121,10 +170,18 @@ __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, 
 // launch shape clSLIC.cpp:307-370.  One workgroup per (superpixel, view).
 __device__ __forceinline__ float wave_tree(float v0, float v1, float v2, float v3) {
   // local_idx k = lane + 64*m holds v_m.  stride 128: k<128 gets k+128; stride
-  // 64: k<64 gets k+64; strides 32..1 stay inside the wave.
+  // 64: k<64 gets k+64; strides 32..1 stay inside the wave, lane k adding lane
+  // k+i without LDS: v_permlane32_swap (i=32), v_permlane16_swap (i=16), DPP
+  // row_shl:i (i=8..1).  Only lane 0's result is used.
   float s = (v0 + v2) + (v1 + v3);
-#pragma unroll
-  for (int i = 32; i >= 1; i >>= 1) s = s + __shfl_down(s, (unsigned)i, 64);
+  unsigned u = __float_as_uint(s);
+  s = s + __uint_as_float(__builtin_amdgcn_permlane32_swap(u, u, false, false)[1]);
+  u = __float_as_uint(s);
+  s = s + __uint_as_float(__builtin_amdgcn_permlane16_swap(u, u, false, false)[1]);
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x108, 0xf, 0xf, true));
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x104, 0xf, 0xf, true));
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x102, 0xf, 0xf, true));
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x101, 0xf, 0xf, true));
   return s;
 }
 
@@ -342,8 +399,9 @@ int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labe
 int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
                   float col_n, float weight, uint32_t* labels) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
-  hipLaunchKernelGGL(k_assign, dim3((W + 63) / 64, (H + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, spixl, W,
-                     H, S, mw, mh, xy_n, col_n, weight, labels);
+  if ((AS_TW / S + 4) * (AS_TH / S + 4) > AS_MAXC) return arg_fail("SLIC assign: spixl_size too small");
+  hipLaunchKernelGGL(k_assign, dim3((W + AS_TW - 1) / AS_TW, (H + AS_TH - 1) / AS_TH, V), dim3(256), 0, s,
+                     (const float4*)lab, spixl, W, H, S, mw, mh, xy_n, col_n, weight, labels);
   MVS_LAUNCH_CHECK("k_assign");
   return 0;
 }

@@ -249,3 +249,25 @@ def test_full_size_slic_properties(engine):
     # one view against the oracle at full size
     olab, osp, olb = orc.slic(stack[0], 32)
     assert_bits(lbh[0], olb, "1080p labels")
+
+
+@pytest.mark.parametrize("kind", ["flat", "ramp", "checker"])
+def test_slic_ties(engine, kind):
+    """Images built so that many pixels sit at (near-)equal distance from two
+    candidate centres: the assignment's strict-< first-wins tie rule and the
+    lazily evaluated square roots must still give the oracle's labels."""
+    H, W, S = 96, 128, 16
+    y, x = np.mgrid[0:H, 0:W]
+    if kind == "flat":
+        img = np.full((H, W, 3), 120, np.uint8)
+    elif kind == "ramp":
+        img = np.stack([(x * 2) % 256, (y * 2) % 256, ((x + y) // 2) % 256], -1).astype(np.uint8)
+    else:
+        img = np.where(((x // 8 + y // 8) % 2)[..., None] == 0, 40, 200).astype(np.uint8).repeat(3, -1)
+    rgbx = np.concatenate([img, np.zeros((H, W, 1), np.uint8)], -1)[None]
+    lab, _ = engine.cvt(dev(rgbx))
+    for S_ in (S, 32, 8):
+        sp, lb = engine.slic(lab, S_)
+        _, osp, olb = orc.slic(rgbx[0], S_)
+        assert_bits(as_u32(lb)[0], olb, f"{kind} labels S={S_}")
+        assert_bits(sp.cpu().numpy()[0][..., :7], osp[..., :7], f"{kind} spixl S={S_}")

@@ -59,17 +59,32 @@ struct SweepArgs {
   float bl;
 };
 
+// One workgroup = 4 waves; each superpixel is shared by wps waves (wps =
+// ceil(D/64) up to 4), wave h taking levels lane + 64 (h + wps p), and all
+// reference views of the call run in one launch (blockIdx.y), so the GPU is
+// filled even at a few thousand superpixels per view.  The per-wave first
+// minima are combined in (cost, index) lexicographic order -- the reference's
+// strict-< scan over levels in index order -- through LDS.
 __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ lab, float* __restrict__ spixl,
                                                      const uint8_t* __restrict__ rep,
                                                      const float* __restrict__ levels, const int* __restrict__ vs,
-                                                     const int* __restrict__ sn, SweepArgs a) {
+                                                     const int* __restrict__ sn, SweepArgs a, int wps) {
   __shared__ float4 refc[4][25];
   __shared__ int2 refxy[4][25];
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  long M = (long)a.mw * a.mh, P = (long)a.W * a.H;
-  long s = (long)blockIdx.x * 4 + w;
-  bool active = s < M;
-  long idx = a.z * M + (active ? s : 0);
+  __shared__ float wbest[4];
+  __shared__ int wbi[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int spb = 4 / wps, h = w % wps;
+  const int z = a.z + blockIdx.y;
+  const long M = (long)a.mw * a.mh, P = (long)a.W * a.H;
+  // XCD-aware order: blocks are dealt round-robin over the 8 XCDs; give each
+  // XCD a contiguous run of superpixels so the neighbour rows its gathers
+  // touch are shared within one L2 instead of being fetched by all eight
+  const long nb = (M + spb - 1) / spb, per = (nb + 7) / 8;
+  const long blk = (long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const long s = blk * spb + w / wps;
+  const bool active = blk < nb && s < M && w / wps < spb;
+  const long idx = z * M + (active ? s : 0);
   const uint8_t* dr = rep + 8 * idx;
   int bl_ = max((int)dr[0], max((int)dr[1], (int)dr[2]));
   int br_ = max((int)dr[5], max((int)dr[6], (int)dr[7]));
@@ -78,7 +93,7 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
   float stx = (float)fmax(1.0, 0.25 * (double)(float)(bl_ + br_));
   float sty = (float)fmax(1.0, 0.25 * (double)(float)(bt_ + bb_));
   float cx = spixl[8 * idx + 1], cy = spixl[8 * idx + 2];
-  const float4* labz = lab + (long)a.z * P;
+  const float4* labz = lab + (long)z * P;
   if (lane < 25) {
     int i = lane / 5 - 2, j = lane % 5 - 2;  // tap order: i (x) outer, j (y) inner
     int xr = (int)(cx + (float)i * stx);
@@ -88,15 +103,15 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
     refc[w][lane] = in ? labz[(long)yr * a.W + xr] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
-  int rx = a.z % a.aw, ry = a.z / a.aw;
-  int nn = sn[a.z];
+  int rx = z % a.aw, ry = z / a.aw;
+  int nn = sn[z];
   float best = 1000000.0f;
   int bi = 0x7fffffff;
-  for (int dl = lane; dl < a.D; dl += 64) {
+  for (int dl = lane + 64 * h; dl < a.D; dl += 64 * wps) {
     float d = levels[dl];
     float mn = 1000000.0f;
     for (int n = 0; n < nn; n++) {
-      int view = vs[a.V * a.z + n];
+      int view = vs[a.V * z + n];
       int vx = view % a.aw, vy = view / a.aw;
       float fdx = d * (float)(vx - rx);
       float fdy = (a.bl * d) * (float)(vy - ry);
@@ -134,7 +149,22 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       bi = oi;
     }
   }
-  if (active && lane == 0) spixl[8 * idx + 7] = (bi != 0x7fffffff && best < 1000000.0f) ? levels[bi] : 0.0f;
+  if (lane == 0) {
+    wbest[w] = best;
+    wbi[w] = bi;
+  }
+  __syncthreads();
+  if (active && h == 0 && lane == 0) {
+    for (int k = 1; k < wps; k++) {
+      const float ob = wbest[w + k];
+      const int oi = wbi[w + k];
+      if (ob < best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    spixl[8 * idx + 7] = (bi != 0x7fffffff && best < 1000000.0f) ? levels[bi] : 0.0f;
+  }
 }
 
 // ---- per-pixel SAD sweep (S=1 grid semantics of initial_depth_estimation_v2)
@@ -305,14 +335,17 @@ int launch_boundary(hipStream_t s, int V, int W, int H, int S, const float* spix
 int launch_sweep_spixl(hipStream_t s, int V, int W, int H, int S, const float* lab, float* spixl,
                        const uint8_t* rep, const float* levels, int D, const int* vs, const int* sn, int aw,
                        float bl, int z0, int z1) {
+  if (z1 <= z0) return 0;
   int mw = map_dim(W, S), mh = map_dim(H, S);
   long M = (long)mw * mh;
-  for (int z = z0; z < z1; z++) {
-    SweepArgs a{V, W, H, mw, mh, D, aw, z, bl};
-    hipLaunchKernelGGL(k_sweep_spixl, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, (const float4*)lab, spixl,
-                       rep, levels, vs, sn, a);
-    MVS_LAUNCH_CHECK("k_sweep_spixl");
-  }
+  int wps = (D + 63) / 64;
+  wps = wps >= 3 ? 4 : wps;  // waves per superpixel: 1, 2 or 4
+  const int spb = 4 / wps;
+  SweepArgs a{V, W, H, mw, mh, D, aw, z0, bl};
+  const long nb = (M + spb - 1) / spb;
+  hipLaunchKernelGGL(k_sweep_spixl, dim3((unsigned)(8 * ((nb + 7) / 8)), (unsigned)(z1 - z0)), dim3(256), 0, s,
+                     (const float4*)lab, spixl, rep, levels, vs, sn, a, wps);
+  MVS_LAUNCH_CHECK("k_sweep_spixl");
   return 0;
 }
 

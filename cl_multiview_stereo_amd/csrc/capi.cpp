@@ -445,4 +445,22 @@ int mvs_do_refinement(mvs_ctx* c, int W, int H, int S, const float* spixl, const
   return 0;
 }
 
+int mvs_do_consistency_filter(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, float fuse,
+                              const float* disp_full, float* out) {
+  if (!c || !disp_full || !out || V <= 0 || array_width <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_do_consistency_filter: bad arguments");
+  size_t n = (size_t)V * W * H * sizeof(float);
+  DevBuf din, dproj, dout;
+  RC(din.alloc(n));
+  RC(dproj.alloc(n));
+  RC(dout.alloc(n));
+  hipStream_t s = c->stream;
+  MVS_HIP(hipMemcpyAsync(din.p, disp_full, n, hipMemcpyHostToDevice, s), "H2D disparity");
+  RC(mvs_filter_d(c, V, W, H, array_width, bl_ratio, fuse, din.as<float>(), dproj.as<float>(), dout.as<float>(), 0,
+                  V));
+  MVS_HIP(hipMemcpyAsync(out, dout.p, n, hipMemcpyDeviceToHost, s), "D2H filtered");
+  MVS_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
 }  // extern "C"

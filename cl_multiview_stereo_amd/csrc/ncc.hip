@@ -303,13 +303,21 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
         read_rows<NR, BW, false>(npk + colo + lane, rows & 0xffff, pv);
       // prefix sums over band rows of the horizontal K-tap correlation: the
       // dot4 accumulator input carries the running sum (exact integers)
+      // (two independent chains over the upper and lower halves of the band
+      // rows, joined by one add each, for twice the instruction-level parallelism)
+      constexpr int NH = NR / 2;
       int ps[NR];
-      unsigned acc = 0u;
+      unsigned acc0 = 0u, acc1 = 0u;
 #pragma unroll
-      for (int k = 0; k < NR; k++) {
-        acc = __builtin_amdgcn_udot4(qhi[k], pv[k].y, __builtin_amdgcn_udot4(qlo[k], pv[k].x, acc, false), false);
-        ps[k] = (int)acc;
+      for (int k = 0; k < NH; k++) {
+        acc0 = __builtin_amdgcn_udot4(qhi[k], pv[k].y, __builtin_amdgcn_udot4(qlo[k], pv[k].x, acc0, false), false);
+        acc1 = __builtin_amdgcn_udot4(qhi[k + NH], pv[k + NH].y,
+                                      __builtin_amdgcn_udot4(qlo[k + NH], pv[k + NH].x, acc1, false), false);
+        ps[k] = (int)acc0;
+        ps[k + NH] = (int)acc1;
       }
+#pragma unroll
+      for (int k = NH; k < NR; k++) ps[k] += ps[NH - 1];
       u32x2 sv[TH];
       if (EVEN)
         read_rows<TH, BW, true>(nst + colo + lane, rows >> 16, sv);

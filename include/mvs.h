@@ -167,6 +167,12 @@ int mvs_do_refinement(mvs_ctx* ctx, int W, int H, int S, const float* spixl, con
                       const uint8_t* rep, const mvs_array* a, const mvs_refine_params* p, float* state_out,
                       float* disp);
 
+/* project_to_reference_inv + remove_view_inconsistency over all V views
+ * (clcode.cl:1995-2101; the reference's disabled call site
+ * depth_refinement.cpp:1398-1451), host pointers [V][H][W]. */
+int mvs_do_consistency_filter(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, float fuse,
+                              const float* disp_full, float* out);
+
 #ifdef __cplusplus
 }
 #endif

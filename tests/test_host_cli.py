@@ -1,0 +1,118 @@
+"""mvs_cli -- the C++ host pipeline (reference clMVDE main + pipeline +
+loader/writer) on libmvs.so.  CPU: its PNG codec on every colour type and
+scanline filter, and argument/file errors.  GPU: a full run on a rendered
+camera-array stack written as PNG files must give the oracle's fused depth
+maps bit-for-bit, and its 8-bit maps the reference's plot scaling."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from pngio import read_png_gray, write_png
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "cl_multiview_stereo_amd", "mvs_cli")
+
+
+@pytest.fixture(scope="module")
+def cli():
+    if not os.path.exists(CLI):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "cl_multiview_stereo_amd", "csrc")], check=True)
+    return CLI
+
+
+@pytest.mark.parametrize("ctype", [0, 2, 4, 6])
+@pytest.mark.parametrize("filt", [0, 1, 2, 3, 4, "mixed"])
+def test_png_decode(cli, tmp_path, ctype, filt):
+    rng = np.random.default_rng(ctype * 10 + (5 if filt == "mixed" else filt))
+    H, W = 13, 37
+    ch = {0: 1, 2: 3, 4: 2, 6: 4}[ctype]
+    px = rng.integers(0, 256, (H, W, ch), dtype=np.uint8)
+    px[3:6, 4:20] = 17  # flat runs exercise the predictors differently
+    src = tmp_path / "in.png"
+    write_png(str(src), px, ctype, filt)
+    out = tmp_path / "out.raw"
+    r = subprocess.run([cli, "--png-decode", str(src), str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == [str(W), str(H)]
+    got = np.fromfile(out, np.uint8).reshape(H, W, 4)
+    want = np.zeros((H, W, 4), np.uint8)
+    if ch <= 2:
+        want[..., 0] = want[..., 1] = want[..., 2] = px[..., 0]
+    else:
+        want[..., :3] = px[..., :3]  # s0 = R (loadImageIn packing)
+    assert np.array_equal(got, want)
+
+
+def test_png_encode_gray(cli, tmp_path):
+    g = (np.arange(19 * 23) % 256).astype(np.uint8).reshape(19, 23)
+    raw = tmp_path / "g.raw"
+    g.tofile(raw)
+    out = tmp_path / "g.png"
+    r = subprocess.run([cli, "--png-encode-gray", "23", "19", str(raw), str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(read_png_gray(str(out)), g)
+
+
+def test_errors(cli, tmp_path):
+    r = subprocess.run([cli, "--data", str(tmp_path / "missing.txt"), "--array", "2x1"], capture_output=True,
+                       text=True)
+    assert r.returncode == 1 and "cannot open" in r.stderr
+    r = subprocess.run([cli, "--bogus"], capture_output=True, text=True)
+    assert r.returncode == 2
+    bad = tmp_path / "bad.png"
+    bad.write_bytes(b"not a png")
+    r = subprocess.run([cli, "--png-decode", str(bad), str(tmp_path / "x")], capture_output=True, text=True)
+    assert r.returncode == 1 and "not a PNG" in r.stderr
+    lst = tmp_path / "one.txt"
+    lst.write_text("a.png\n")
+    r = subprocess.run([cli, "--data", str(lst), "--array", "2x1"], capture_output=True, text=True)
+    assert r.returncode == 1 and "needs 2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_pipeline_matches_oracle(cli, tmp_path):
+    from cl_multiview_stereo_amd import params, synth
+    from oracle import oracle as orc
+    aw, ah, W, H, S, dmin, dmax, bl = 3, 1, 100, 70, 8, 2, 14, 1.0
+    stack, _ = synth.make_stack(W, H, aw, ah, dmin, dmax, bl, 31)
+    names = []
+    for v in range(aw * ah):
+        n = f"img{v}.png"
+        write_png(str(tmp_path / n), stack[v][..., :3], 2, "mixed")
+        names.append(n)
+    (tmp_path / "data.txt").write_text("\n".join(names) + "\n")
+    out = tmp_path / "out"
+    out.mkdir()
+    r = subprocess.run([cli, "--data", str(tmp_path / "data.txt"), "--array", f"{aw}x{ah}", "--spixl-size", str(S),
+                        "--min-disp", str(dmin), "--max-disp", str(dmax), "--bl-ratio", str(bl), "--kernel-size",
+                        "52", "--filter", "--dump-init", "--out", str(out), "--quiet"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    # the oracle on the same images with the same settings
+    outs = [orc.slic(stack[v], S) for v in range(aw * ah)]
+    lab = np.stack([o[0] for o in outs])
+    sp = np.stack([o[1] for o in outs])
+    lb = np.stack([o[2] for o in outs])
+    rep = orc.boundary(sp, lb, S)
+    levels = params.disparity_levels(dmin, dmax, 1)
+    vs, sn = params.flatten_subsets(params.neighbour_lists(aw, ah, 1, 1))
+    sp = orc.sweep(lab, sp, rep, levels, vs, sn, aw, bl, S)
+    ref = orc.refine(sp, lb, rep, vs, sn, aw, bl, S, kernel_size=52)
+    depth = np.fromfile(out / "depth.f32", np.float32).reshape(aw * ah, H, W)
+    assert np.array_equal(depth.view(np.uint32), ref["disp"].view(np.uint32))
+    _, filt = orc.filt(ref["disp"], aw, bl, 1.0)
+    got_f = np.fromfile(out / "filtered.f32", np.float32).reshape(aw * ah, H, W)
+    assert np.array_equal(got_f.view(np.uint32), filt.view(np.uint32))
+    for v in range(aw * ah):
+        g = read_png_gray(str(out / f"fus {v}.png"))
+        want = np.clip(np.floor((ref["disp"][v] - np.float32(dmin)) / np.float32(dmax - dmin) * np.float32(255)),
+                       0, 255).astype(np.uint8)
+        assert np.array_equal(g, want)
+        init = read_png_gray(str(out / f"init {v}.png"))
+        s7 = sp[v].reshape(-1, 8)[lb[v].reshape(-1), 7].reshape(H, W)
+        want_i = np.clip(np.floor((s7 - np.float32(dmin)) / np.float32(dmax - dmin) * np.float32(255)), 0,
+                         255).astype(np.uint8)
+        assert np.array_equal(init, want_i)

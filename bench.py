@@ -33,6 +33,13 @@ CONFIGS = {
                workload="2-view 640x480, 32 hypotheses, SAD 5x5, SLIC off (reference per-pixel sweep)"),
     "c2": dict(aw=5, ah=1, W=1920, H=1080, S=32, dmin=0, dmax=127, K=5, nh=4, nv=0, bl=1.0, cost="ncc",
                workload="5-view 1920x1080, 128 hypotheses, NCC 5x5, SLIC K=2040 (S=32), 1 GPU per 5-view stack"),
+    "c3": dict(aw=5, ah=1, W=1920, H=1080, S=32, dmin=0, dmax=127, K=5, nh=4, nv=0, bl=1.0, cost="ncc",
+               refine=True, filt=True,
+               workload="C2 + superpixel refinement (5 propagations) + cross-view consistency filter, 1 GPU per stack"),
+    "c4": dict(aw=8, ah=4, W=1920, H=1080, S=32, dmin=0, dmax=127, K=5, nh=0, nv=0, knn=5, bl=1.0, cost="ncc",
+               refine=True, filt=True, sharded=True,
+               workload="32 reference views x 5 nearest neighbours, 1080p, one array sharded by reference view over "
+                        "the GPUs (RCCL all-gathers of labels/spixl, refinement state, disparity)"),
     "c5": dict(aw=5, ah=1, W=4096, H=3072, S=40, dmin=0, dmax=255, K=7, nh=4, nv=0, bl=1.0, cost="ncc",
                workload="5-view 4096x3072, 256 hypotheses, NCC 7x7, SLIC K=7931 (S=40)"),
 }
@@ -76,10 +83,18 @@ def main():
     D = cfg["dmax"] - cfg["dmin"] + 1
 
     e = Engine(local)
+    sharded = bool(cfg.get("sharded"))
+    # independent stacks per rank (weak scaling) or one array sharded by view (strong)
     stack, _ = synth.make_stack(W, H, cfg["aw"], cfg["ah"], cfg["dmin"], cfg["dmax"], cfg["bl"],
-                                0x5EED + 2 + rank)
+                                0x5EED + 2 + (0 if sharded else rank))
     rgbx = torch.from_numpy(stack).to(e.device)
-    pipe = Pipeline(e, st, W, H, pixel_cost=cost)
+    vlists = (params.nearest_neighbours(cfg["aw"], cfg["ah"], cfg["knn"]) if cfg.get("knn") else None)
+    pipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=cost, refine=bool(cfg.get("refine")),
+                    filt=bool(cfg.get("filt")) and not sharded)
+    if sharded:
+        from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
+        spipe = ShardedPipeline(EngineBackend(e), st, pipe.cam, ViewGather(V), pixel_cost=cost, refine=True,
+                                filt=bool(cfg.get("filt")))
 
     # HIP events around the cost-volume kernels, on the stream they run on
     timers = {"wta": [], "ncc": []}
@@ -104,7 +119,7 @@ def main():
         timing = [False]
 
     def step():
-        return pipe.exe_pipeline(rgbx)
+        return spipe.run(rgbx) if sharded else pipe.exe_pipeline(rgbx)
 
     for _ in range(args.warmup):
         step()
@@ -127,7 +142,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed * 1e3 / max(args.steps, 1)
-    mpix = world * V * W * H * args.steps / elapsed / 1e6
+    units = V if sharded else world * V  # reference views processed per step, whole job
+    mpix = units * W * H * args.steps / elapsed / 1e6
 
     res = {
         "metric": "Mpix/s depth (1080p, 128 depth hyp, 5 views) + depth L1 vs ref",
@@ -138,13 +154,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "f32/i32",
         "data": "synthetic (seeded rendered camera-array stack, RGBx resident in HBM)",
         "config": {"workload": cfg["workload"], "views": V, "width": W, "height": H, "hypotheses": D,
-                   "window": cfg["K"], "cost": cost, "spixl_size": cfg["S"], "neighbours": cfg["nh"],
-                   "parallelism": f"view-stack per GPU x{world}"},
+                   "window": cfg["K"], "cost": cost, "spixl_size": cfg["S"],
+                   "neighbours": int(pipe.cam.subset_num.max()),
+                   "parallelism": (f"views sharded over {world} GPU(s)" if sharded else
+                                   f"view-stack per GPU x{world}"),
+                   "refinement": bool(cfg.get("refine")), "consistency_filter": bool(cfg.get("filt"))},
     }
 
     if timers["wta"]:
@@ -166,7 +185,7 @@ def main():
                            "traffic": traffic, "algorithmic_bytes_per_launch": wta_bytes,
                            "avg_launch_ms": round(t_wta * 1e3, 4)}
         cells = float(D) * W * H
-        nbr = cfg["nh"] if cfg["aw"] > 1 else 1
+        nbr = max(1, int(pipe.cam.subset_num[0]))
         vol_bytes = 4.0 * cells
         res["roofline_sweep"] = {"kernel": "k_ncc_volume (cost-volume write pass)", "avg_launch_ms": round(t_ncc * 1e3, 4),
                                  "view_cells_per_s": round(cells * nbr / t_ncc / 1e9, 3),
@@ -174,7 +193,7 @@ def main():
                                  "hbm_write_GBps": round(vol_bytes / t_ncc / 1e9, 1),
                                  "hbm_write_frac": round(vol_bytes / t_ncc / 1e9 / HBM_PEAK_GBS, 4)}
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg.get("refine"):
         try:
             res["cpu_baseline"], res["depth_l1_vs_oracle"] = cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out)
         except Exception as ex:  # report, never hide

@@ -269,62 +269,31 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
   return finish_consistency(cons, vc);
 }
 
-// update, clcode.cl:1635-1673
-__device__ void plane_update(const PCtx& p, long q, PState& cur) {
-  const float* s1 = p.st + 6 * q;
-  float nx = s1[3], ny = s1[4], nz = s1[5], d1 = s1[0];
-  const float* sc = p.spixl + 8 * q;
-  float t = nx * (sc[1] - p.cx);
-  t = t + ny * (sc[2] - p.cy);
-  t = t + nz * d1;
-  float di = t / nz;
-  float sm1 = comp_smoothness(p, di, nx, ny, nz);
-  float cs1 = comp_consistency(p, di, nx, ny, nz);
-  float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], sc[3], sc[4], sc[5]);
-  float simi = expf_neg_sq(diff, p.c.gamma);
-  if ((p.iter < 4 && sm1 * simi > cur.sm) || cs1 * sm1 > cur.sm * cur.cs) {
-    cur.d = di; cur.sm = sm1; cur.cs = cs1; cur.nx = nx; cur.ny = ny; cur.nz = nz;
-  }
+// One WAVE per superpixel.  The reference evaluates its candidate planes one
+// after another, but a candidate's (sm, cs) never depends on the running
+// state -- only the accept test does -- so lanes evaluate the candidates in
+// parallel (plane candidates in batches of 64, then the 8 spatial-refinement
+// triangles, whose normals use the post-plane depth) and the accept tests run
+// in the reference's order over the broadcast results: bit-identical, with
+// the superpixel count of waves in flight instead of that many threads.
+// k is wave-uniform at every call: a v_readlane into an SGPR, not an LDS permute
+__device__ __forceinline__ float bcast(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
-// spatialRefinement + cross_product_test + normalize, clcode.cl:1676-1723
-__device__ void spatial_refine(const PCtx& p, int ax, int ay, int bx, int by, PState& cur) {
-  const RArgs& c = p.c;
-  long M = (long)c.mw * c.mh;
-  long q1 = M * p.z + (long)c.mw * ay + ax, q2 = M * p.z + (long)c.mw * by + bx;
-  const float* a1 = p.spixl + 8 * q1;
-  const float* a2 = p.spixl + 8 * q2;
-  float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = p.st[6 * q1] - cur.d;
-  float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = p.st[6 * q2] - cur.d;
-  float n0 = v1y * v2z - v1z * v2y;
-  float n1 = v2x * v1z - v1x * v2z;
-  float n2 = v1x * v2y - v1y * v2x;
-  float n3 = 0.0f;
-  float s = n0 * n0;
-  s = s + n1 * n1;
-  s = s + n2 * n2;
-  s = s + n3 * n3;
-  if (s != 0.0f) {
-    float r = sqrtf(s);
-    n0 = n0 / r; n1 = n1 / r; n2 = n2 / r;
-  }
-  float sm1 = comp_smoothness(p, cur.d, n0, n1, n2);
-  float cs1 = comp_consistency(p, cur.d, n0, n1, n2);
-  if ((p.iter < 4 && sm1 > cur.sm) || sm1 * cs1 > cur.sm * cur.cs) {
-    cur.sm = sm1; cur.cs = cs1; cur.nx = n0; cur.ny = n1; cur.nz = n2;
-  }
-}
-
-__global__ __launch_bounds__(128) void k_propagate(RArgs c, const float* __restrict__ spixl,
+__global__ __launch_bounds__(256) void k_propagate(RArgs c, const float* __restrict__ spixl,
                                                    const uint32_t* __restrict__ labels,
                                                    const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
                                                    const int* __restrict__ vs, const int* __restrict__ sn, int iter,
                                                    int nks, float kss, const float* __restrict__ st_in,
-                                                   float* __restrict__ st_out, int z0) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = z0 + blockIdx.z;
-  if (x >= c.mw) return;
-  long M = (long)c.mw * c.mh;
-  long idx = M * z + (long)c.mw * y + x;
+                                                   float* __restrict__ st_out, int z0, long nsp) {
+  const int lane = threadIdx.x & 63;
+  const long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nsp) return;  // whole wave; no barriers in this kernel
+  const long M = (long)c.mw * c.mh;
+  const int z = z0 + (int)(g / M);
+  const int x = (int)(g % M) % c.mw, y = (int)(g % M) / c.mw;
+  const long idx = M * z + (long)c.mw * y + x;
   PCtx p;
   p.c = c; p.spixl = spixl; p.labels = labels; p.vs = vs; p.sn = sn; p.st = st_in;
   p.x = x; p.y = y; p.z = z; p.iter = iter; p.nks = nks; p.kss = kss;
@@ -334,30 +303,144 @@ __global__ __launch_bounds__(128) void k_propagate(RArgs c, const float* __restr
   samples_of(rep + 8 * idx, p.smp);
   const float* si = st_in + 6 * idx;
   PState cur{si[0], si[1], si[2], si[3], si[4], si[5]};
-  for (int i = -1; i <= 1; i++)
-    for (int j = -1; j <= 1; j++) {
-      int px = x + i, py = y + j;
-      if (px >= 0 && py >= 0 && px < c.mw && py < c.mh && !(i == 0 && j == 0))
-        plane_update(p, M * z + (long)c.mw * py + px, cur);
+
+  // compute_smoothness terms (clcode.cl:1407-1470) whose neighbour, colour
+  // similarity and neighbour depth do not depend on the candidate plane: lane t
+  // holds term t (the 8 neighbours, then left/right/up/down at each far step),
+  // computed once; each candidate then only evaluates its plane at the
+  // neighbour centres.  Sums keep the reference's term order.
+  const int ss = step_size_of(p.fl.x, kss);
+  const int nterm = 9 + 4 * nks;
+  const bool fast_sm = nterm <= 64;
+  float t_simi = 0.f, t_sx = 0.f, t_sy = 0.f, t_sd = 0.f, wn = 0.f;
+  unsigned long long t_valid = 0ull;
+  if (fast_sm) {
+    long q = -1;
+    float gi = c.gamma;
+    const int k = lane;
+    if (k < 9) {
+      const int i = k / 3 - 1, j = k % 3 - 1, px = x + i, py = y + j;
+      if (px >= 0 && py >= 0 && px < c.mw && py < c.mh && (i != 0 || j != 0)) q = M * z + (long)c.mw * py + px;
+    } else if (k < nterm) {
+      const int i = (k - 9) / 4 + 1, dir = (k - 9) % 4, step = i * ss;
+      gi = c.gamma * (float)(1 + i);
+      const int qx[4] = {x - (step + 1), x + (step + 1), x, x};
+      const int qy[4] = {y, y, y - (step + 1), y + (step + 1)};
+      const bool ok[4] = {x > step, x < c.mw - step - 1, y > step, y < c.mh - step - 1};
+      if (ok[dir]) q = M * z + (long)c.mw * qy[dir] + qx[dir];
     }
-  int ssz = (int)kss;
-  for (int i = 1; i <= nks; i++) {
-    int off = i * ssz;
-    if (y > off) plane_update(p, M * z + (long)c.mw * (y - (off + 1)) + x, cur);
-    if (y < c.mh - off - 1) plane_update(p, M * z + (long)c.mw * (y + off + 1) + x, cur);
-    if (x > off) plane_update(p, M * z + (long)c.mw * y + (x - off - 1), cur);
-    if (x < c.mw - off - 1) plane_update(p, M * z + (long)c.mw * y + (x + off + 1), cur);
+    if (q >= 0) {
+      const float* sq = spixl + 8 * q;
+      // neighbour terms: distance(own colour, neighbour); far terms the reverse (same bits)
+      const float diff = k < 9 ? mvs_distance3(p.col[0], p.col[1], p.col[2], sq[3], sq[4], sq[5])
+                               : mvs_distance3(sq[3], sq[4], sq[5], p.col[0], p.col[1], p.col[2]);
+      t_simi = expf_neg_sq(diff, gi);
+      t_sx = sq[1];
+      t_sy = sq[2];
+      t_sd = st_in[6 * q];
+    }
+    t_valid = __ballot(q >= 0);
+    for (int l = 0; l < nterm; l++)
+      if ((t_valid >> l) & 1ull) wn = wn + bcast(t_simi, l);
   }
-  const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
-  const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
-  for (int i = 0; i < 8; i++) {
-    int j = (i + 1) % 8;
-    if (nbx[i] > -1 && nby[i] > -1 && nbx[i] < c.mw && nby[i] < c.mh && nbx[j] > -1 && nby[j] > -1 &&
-        nbx[j] < c.mw && nby[j] < c.mh)
-      spatial_refine(p, nbx[i], nby[i], nbx[j], nby[j], cur);
+  auto smooth = [&](float d, float nx, float ny, float nz) -> float {
+    if (!fast_sm) return comp_smoothness(p, d, nx, ny, nz);
+    float sm = 0.0f;
+    for (int l = 0; l < nterm; l++) {
+      if (!((t_valid >> l) & 1ull)) continue;
+      const float di = plane_at(nx, ny, nz, p.cx, p.cy, d, bcast(t_sx, l), bcast(t_sy, l));
+      const float diff = di - bcast(t_sd, l);
+      sm = sm + bcast(t_simi, l) * expf_neg_sq(diff, c.alpha);
+    }
+    return wn > 0 ? sm / wn : 0.000001f;
+  };
+
+  // plane candidates in the reference order (clcode.cl:1772-1805): the 8
+  // neighbours, then for i = 1..nks up, down, left, right at offset i*(int)kss
+  const int ssz = (int)kss;
+  auto cand = [&](int k) -> long {  // superpixel of candidate slot k, -1 if out of the map
+    if (k < 9) {
+      const int i = k / 3 - 1, j = k % 3 - 1, px = x + i, py = y + j;
+      return (px >= 0 && py >= 0 && px < c.mw && py < c.mh && !(i == 0 && j == 0)) ? M * z + (long)c.mw * py + px
+                                                                                     : -1;
+    }
+    const int i = (k - 9) / 4 + 1, dir = (k - 9) % 4, off = i * ssz;
+    if (dir == 0) return y > off ? M * z + (long)c.mw * (y - (off + 1)) + x : -1;
+    if (dir == 1) return y < c.mh - off - 1 ? M * z + (long)c.mw * (y + off + 1) + x : -1;
+    if (dir == 2) return x > off ? M * z + (long)c.mw * y + (x - off - 1) : -1;
+    return x < c.mw - off - 1 ? M * z + (long)c.mw * y + (x + off + 1) : -1;
+  };
+  const int nslot = 9 + 4 * nks;
+  for (int b = 0; b < nslot; b += 64) {
+    const int k = b + lane;
+    const long q = k < nslot ? cand(k) : -1;
+    float di = 0.f, sm1 = 0.f, cs1 = 0.f, simi = 0.f, nx = 0.f, ny = 0.f, nz = 1.f;
+    if (q >= 0) {  // update(), clcode.cl:1635-1673, minus the accept test
+      const float* s1 = st_in + 6 * q;
+      nx = s1[3]; ny = s1[4]; nz = s1[5];
+      const float* sc = spixl + 8 * q;
+      float t = nx * (sc[1] - p.cx);
+      t = t + ny * (sc[2] - p.cy);
+      t = t + nz * s1[0];
+      di = t / nz;
+      sm1 = smooth(di, nx, ny, nz);
+      cs1 = comp_consistency(p, di, nx, ny, nz);
+      const float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], sc[3], sc[4], sc[5]);
+      simi = expf_neg_sq(diff, c.gamma);
+    }
+    const unsigned long long valid = __ballot(q >= 0);
+    for (int l = 0; l < 64 && b + l < nslot; l++) {  // accept tests in order, on every lane
+      if (!((valid >> l) & 1ull)) continue;
+      const float ksm = bcast(sm1, l), kcs = bcast(cs1, l), ksi = bcast(simi, l);
+      if ((iter < 4 && ksm * ksi > cur.sm) || kcs * ksm > cur.sm * cur.cs) {
+        cur.d = bcast(di, l); cur.sm = ksm; cur.cs = kcs;
+        cur.nx = bcast(nx, l); cur.ny = bcast(ny, l); cur.nz = bcast(nz, l);
+      }
+    }
   }
-  float* o = st_out + 6 * idx;
-  o[0] = cur.d; o[1] = cur.sm; o[2] = cur.cs; o[3] = cur.nx; o[4] = cur.ny; o[5] = cur.nz;
+
+  // spatialRefinement over the 8 neighbour triangles (clcode.cl:1676-1723, 1808-1820)
+  {
+    const int t = lane & 7;
+    const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
+    const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
+    const int u = (t + 1) % 8;
+    const bool ok = lane < 8 && nbx[t] > -1 && nby[t] > -1 && nbx[t] < c.mw && nby[t] < c.mh && nbx[u] > -1 &&
+                    nby[u] > -1 && nbx[u] < c.mw && nby[u] < c.mh;
+    float sm1 = 0.f, cs1 = 0.f, n0 = 0.f, n1 = 0.f, n2 = 0.f;
+    if (ok) {
+      const long q1 = M * z + (long)c.mw * nby[t] + nbx[t], q2 = M * z + (long)c.mw * nby[u] + nbx[u];
+      const float* a1 = spixl + 8 * q1;
+      const float* a2 = spixl + 8 * q2;
+      const float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = st_in[6 * q1] - cur.d;
+      const float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = st_in[6 * q2] - cur.d;
+      n0 = v1y * v2z - v1z * v2y;
+      n1 = v2x * v1z - v1x * v2z;
+      n2 = v1x * v2y - v1y * v2x;
+      float ss = n0 * n0;
+      ss = ss + n1 * n1;
+      ss = ss + n2 * n2;
+      ss = ss + 0.0f * 0.0f;
+      if (ss != 0.0f) {
+        const float r = sqrtf(ss);
+        n0 = n0 / r; n1 = n1 / r; n2 = n2 / r;
+      }
+      sm1 = smooth(cur.d, n0, n1, n2);
+      cs1 = comp_consistency(p, cur.d, n0, n1, n2);
+    }
+    const unsigned long long valid = __ballot(ok);
+    for (int l = 0; l < 8; l++) {
+      if (!((valid >> l) & 1ull)) continue;
+      const float ksm = bcast(sm1, l), kcs = bcast(cs1, l);
+      if ((iter < 4 && ksm > cur.sm) || ksm * kcs > cur.sm * cur.cs) {
+        cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, l); cur.ny = bcast(n1, l); cur.nz = bcast(n2, l);
+      }
+    }
+  }
+  if (lane == 0) {
+    float* o = st_out + 6 * idx;
+    o[0] = cur.d; o[1] = cur.sm; o[2] = cur.cs; o[3] = cur.nx; o[4] = cur.ny; o[5] = cur.nz;
+  }
 }
 
 // ---- spixl_to_image ----------------------------------------------------------
@@ -459,8 +542,9 @@ int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl
                      const float* st_in, float* st_out, int z0, int z1) {
   if (z1 <= z0) return 0;
   RArgs c{V, W, H, S, map_dim(W, S), map_dim(H, S), aw, bl, fuse, alpha, gamma};
-  hipLaunchKernelGGL(k_propagate, dim3((c.mw + 63) / 64, c.mh, z1 - z0), dim3(64), 0, s, c, spixl, labels, rep,
-                     (const float2*)flat, vs, sn, iter, nks, kss, st_in, st_out, z0);
+  const long nsp = (long)c.mw * c.mh * (z1 - z0);
+  hipLaunchKernelGGL(k_propagate, dim3((unsigned)((nsp + 3) / 4)), dim3(256), 0, s, c, spixl, labels, rep,
+                     (const float2*)flat, vs, sn, iter, nks, kss, st_in, st_out, z0, nsp);
   MVS_LAUNCH_CHECK("k_propagate");
   return 0;
 }

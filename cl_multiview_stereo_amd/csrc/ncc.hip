@@ -7,15 +7,18 @@
 // the image; with n = K*K and integer sums
 //   num = n*Srp - Sr*Sp,  vr = n*Srr - Sr^2,  vp = n*Spp - Sp^2
 // ivr = vr ? 1/(float)vr : 0 and ivp likewise (per pixel),
-// e_n = ((a*|a|)*ivr)*ivp with a = (float)num (signed squared NCC) for valid
-// windows; vol[d][y][x] = 1 - max(-1, max over valid neighbours e_n): 1 minus
-// the best signed squared correlation, 2 when no neighbour window is valid.
+// e_n = (a*|a|)*ivp with a = (float)num for valid windows, m = max_n e_n
+// (-inf if none), vol[d][y][x] = 1 - max(-1, m*ivr): 1 minus the best signed
+// squared correlation, 2 when no neighbour window is valid.  (ivr after the
+// maximum: rounding is monotone, so m*ivr = max_n (e_n*ivr).)  Every sum is
+// invariant under centring the intensities (q - 128), which the planes do.
 //
 // Data layout (mvs_box_stats_d, per view, 16 B/px in two planes):
-//   stats [V][H][W] {S, bits(ivr)}: window sum and reciprocal variance, with
+//   stats [V][H][W] {S', bits(ivr)}: centred window sum S' = S - 128 n (K=5:
+//                   as a float, K=7: as an int) and reciprocal variance, with
 //                   ivr = NaN where the window leaves the image;
-//   pk    [V][H][W] {lo, hi}: the 8 intensities q(x-R .. x-R+7) of row y
-//                   packed little-endian (0 outside the image).
+//   pk    [V][H][W] {lo, hi}: the 8 centred intensities q-128 (int8) of
+//                   columns x-R .. x-R+7 of row y, packed little-endian.
 // Validity is carried by the data: an invalid window anywhere makes e NaN and
 // v_max_f32 (IEEE maxNum) drops it -- no per-cell bounds logic.
 //
@@ -27,11 +30,12 @@
 //     are staged in LDS by 16-byte LDS-DMA (2 px per lane), double-buffered so
 //     the next neighbour's bands land while this one is computed;
 //   * per (level, neighbour) a lane walks its column: per band row one
-//     ds_read_b64 and two v_dot4_u32_u8 give the exact horizontal K-tap
-//     correlation, a register sliding window the vertical K-sum, then 7 VALU
-//     ops finish the cell (integer num, IEEE f32 e, v_max_f32);
+//     ds_read_b64 and two v_dot4_i32_i8 give the exact horizontal K-tap
+//     centred correlation, a prefix sum the vertical K-sum, then 6 VALU ops
+//     finish the cell (num, IEEE f32 e, v_max_f32);
 //   * the chunk's costs are written once, 64-column coalesced rows.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "mvs_internal.h"
@@ -87,14 +91,16 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
     const int var = NK * ss - s * s;
     const float iv = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / (float)var : 0.0f);
     const long o = z * Pv + pair_index(y, x, W);
-    // window sum: K = 5 stores it centred, as a float (S - 128*n, exact), for
-    // the FP32 finish of k_ncc_volume; K = 7 stores the integer S
-    const unsigned sw = R == 2 ? (unsigned)__float_as_int((float)((valid ? s : 0) - 128 * NK)) : (unsigned)(valid ? s : 0);
+    // centred window sum S - 128 n: K = 5 as a float (exact) for the FP32
+    // finish of the sweeps, K = 7 as an int
+    const int sc = (valid ? s : 0) - 128 * NK;
+    const unsigned sw = R == 2 ? (unsigned)__float_as_int((float)sc) : (unsigned)sc;
     stats[o] = make_uint2(sw, (unsigned)__float_as_int(iv));
     const uint8_t* row = &t[ly + R][lx];
     unsigned lo = row[0] | (row[1] << 8) | (row[2] << 16) | ((unsigned)row[3] << 24);
     unsigned hi = row[4] | (row[5] << 8) | (row[6] << 16) | ((unsigned)row[7] << 24);
-    pk[o] = y < H ? make_uint2(lo, hi) : make_uint2(0u, 0u);
+    // q - 128 as int8 is q ^ 0x80
+    pk[o] = y < H ? make_uint2(lo ^ 0x80808080u, hi ^ 0x80808080u) : make_uint2(0u, 0u);
   }
 }
 
@@ -223,13 +229,16 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
     }
   };
   float E[DPW][TH];
+  float ivr[TH];
   auto reset = [&]() {
 #pragma unroll
     for (int j = 0; j < DPW; j++)
 #pragma unroll
-      for (int o = 0; o < TH; o++) E[j][o] = -1.0f;
+      for (int o = 0; o < TH; o++) E[j][o] = -INFINITY;
   };
-  auto store = [&](int c) {  // cost = 1 - E of chunk c's levels; partial tiles/chunks masked
+  // cost = 1 - max(-1, E ivr) of chunk c's levels (v_max_f32 drops the NaN of
+  // -inf * 0 and of an invalid reference window); partial tiles/chunks masked
+  auto store = [&](int c) {
     if (x >= W) return;
 #pragma unroll
     for (int j = 0; j < DPW; j++) {
@@ -239,12 +248,14 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
       const int off0 = y0 * W + x;
 #pragma unroll
       for (int o = 0; o < TH; o++)
-        if (y0 + o < H) vd[off0 + o * W] = 1.0f - E[j][o];
+        if (y0 + o < H) vd[off0 + o * W] = 1.0f - vmax(E[j][o] * ivr[o], -1.0f);
     }
   };
 
   reset();
   if (T == 0) {  // no neighbours: every window invalid, cost 2
+#pragma unroll
+    for (int o = 0; o < TH; o++) ivr[o] = __int_as_float(0x7fc00000);
     for (int c = 0; c < a.nch; c++) store(c);
     return;
   }
@@ -259,25 +270,17 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
     qlo[k] = v.x;
     qhi[k] = v.y & HI_MASK;
   }
-  // K = 5 (FPF): num = n*Srp - Sr*Sp evaluated in FP32 on centred sums
-  //   (Srp_c = Srp - 128(Sr + Sp) + 128^2 n, |n Srp_c|, |Sr_c Sp_c| <= 10.24M),
-  //   every intermediate an integer below 2^24 and one rounding at the final
-  //   fma: bit-identical to (float)num, at the FP32 issue rate (integer VALU
-  //   ops issue at half rate on gfx950).  K = 7 exceeds 2^24: integer finish.
-  // rs[o]: FPF -(Sr_c) as float, else -Sr as int bits;  ar[o]: -128 Sr_c - 128^2 n.
-  float rs[TH], ar[TH];
-  float ivr[TH];
+  // K = 5 (FPF): num = n*Srp' - Sr'*Sp' on centred sums (|n Srp'|,
+  //   |Sr' Sp'| <= 10.24M), every intermediate an integer below 2^24 and one
+  //   rounding at the final fma: bit-identical to (float)num, at the FP32
+  //   issue rate (integer VALU ops issue at half rate on gfx950).  K = 7
+  //   exceeds 2^24: integer finish.
+  // rs[o]: -Sr' (FPF as float, else as int bits)
+  float rs[TH];
 #pragma unroll
   for (int o = 0; o < TH; o++) {
     const uint2 v = stats[zo + pair_index(min(y0 + o, H - 1), xc, W)];
-    if (FPF) {
-      const float src = __int_as_float((int)v.x);
-      rs[o] = -src;
-      ar[o] = -128.0f * src - (float)(128 * 128 * NK);
-    } else {
-      rs[o] = __int_as_float(-(int)v.x);
-      ar[o] = 0.0f;
-    }
+    rs[o] = FPF ? -__int_as_float((int)v.x) : __int_as_float(-(int)v.x);
     ivr[o] = __int_as_float((int)v.y);
   }
   __syncthreads();
@@ -301,20 +304,21 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
         read_rows<NR, BW, true>(npk + colo + lane, rows & 0xffff, pv);
       else
         read_rows<NR, BW, false>(npk + colo + lane, rows & 0xffff, pv);
-      // prefix sums over band rows of the horizontal K-tap correlation: the
-      // dot4 accumulator input carries the running sum (exact integers)
+      // prefix sums over band rows of the horizontal K-tap centred
+      // correlation: the dot4 accumulator input carries the running sum
       // (two independent chains over the upper and lower halves of the band
       // rows, joined by one add each, for twice the instruction-level parallelism)
       constexpr int NH = NR / 2;
       int ps[NR];
-      unsigned acc0 = 0u, acc1 = 0u;
+      int acc0 = 0, acc1 = 0;
 #pragma unroll
       for (int k = 0; k < NH; k++) {
-        acc0 = __builtin_amdgcn_udot4(qhi[k], pv[k].y, __builtin_amdgcn_udot4(qlo[k], pv[k].x, acc0, false), false);
-        acc1 = __builtin_amdgcn_udot4(qhi[k + NH], pv[k + NH].y,
-                                      __builtin_amdgcn_udot4(qlo[k + NH], pv[k + NH].x, acc1, false), false);
-        ps[k] = (int)acc0;
-        ps[k + NH] = (int)acc1;
+        acc0 = __builtin_amdgcn_sdot4((int)qhi[k], (int)pv[k].y,
+                                      __builtin_amdgcn_sdot4((int)qlo[k], (int)pv[k].x, acc0, false), false);
+        acc1 = __builtin_amdgcn_sdot4((int)qhi[k + NH], (int)pv[k + NH].y,
+                                      __builtin_amdgcn_sdot4((int)qlo[k + NH], (int)pv[k + NH].x, acc1, false), false);
+        ps[k] = acc0;
+        ps[k + NH] = acc1;
       }
 #pragma unroll
       for (int k = NH; k < NR; k++) ps[k] += ps[NH - 1];
@@ -333,15 +337,13 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
         float fa;
         if (FPF) {
           const float spc = __int_as_float((int)sv[o].x);
-          const float srp = o > 0 ? pf[o + 2 * R] - pf[o - 1] : pf[2 * R];  // Srp, exact
-          const float src = __builtin_fmaf(-128.0f, spc, srp + ar[o]);     // Srp_c, exact
-          fa = __builtin_fmaf(rs[o], spc, (float)NK * src);                 // (float)num
+          const float srp = o > 0 ? pf[o + 2 * R] - pf[o - 1] : pf[2 * R];  // Srp', exact
+          fa = __builtin_fmaf(rs[o], spc, (float)NK * srp);                 // (float)num
         } else {
           const int srp = o > 0 ? ps[o + 2 * R] - ps[o - 1] : ps[2 * R];
           fa = (float)(__mul24(NK, srp) + __mul24(__float_as_int(rs[o]), (int)sv[o].x));
         }
         float e = fa * fabsf(fa);
-        e = e * ivr[o];
         e = e * __int_as_float((int)sv[o].y);
         E[j][o] = vmax(E[j][o], e);
       }
@@ -354,6 +356,310 @@ __global__ __launch_bounds__(256) void k_ncc_volume(const uint2* __restrict__ st
     n = n1;
     __syncthreads();  // step t+1's bands landed (vmcnt 0); this buffer free for t+2
   }
+}
+
+// ---- matrix-core sweep for horizontal camera arrays -----------------------
+// When every neighbour's shift is horizontal and linear in the level index,
+// tx(l) = t0 + l*delta (integer levels, ty = 0), the centred correlations of
+// one image row are a banded integer GEMM:
+//   Srp'(x_i, c_j) = sum_k A[i][k] B[k][j],  A[i][k] = window tap k of the
+//   reference at pixel x_i,  B[k][j] = tap k of the neighbour at column c_j,
+// and level l of pixel x_i is column c = x_i - t0 - l*delta.  With pixels and
+// columns taken in one residue class mod s = |delta| (x_i = xa + s i,
+// c_j = cb + s j) the needed (i, j) form the diagonal band j - i in
+// [0, D-1] of a 16 x (D+15) tile strip: one v_mfma_i32_16x16x64_i8 per 16 x 16
+// tile (the K x K window as 8-byte rows of the packed plane, K-group h of a
+// lane = one row pair of its 16-byte slot), ~89% of its outputs used at D=128.
+// The per-cell finish is the same FP32/integer arithmetic as k_ncc_volume;
+// the maximum over neighbours is an LDS float max (ds_max_f32) into the
+// workgroup's [level][pixel] tile; cells of the two band-edge N-tiles that
+// fall outside [0, D) are clamped into a dump row on either side.
+//
+// Work: M-tiles (neighbour n, residue rho, tile m; a host table of 16-byte
+// records, one per lane, read back with v_readlane) dealt round-robin to the
+// 4 waves; a wave loads an M-tile's reference operand and row sums once and
+// walks its N-tiles nt = 0 .. NT-1 (the band), prefetching the next N-tile's
+// neighbour operand while the current one is multiplied and finished.
+constexpr int MF_X = 64;      // pixels per workgroup tile (one image row)
+constexpr int MF_PITCH = 65;  // LDS row pitch (floats)
+constexpr int MF_LOFF = 1;    // dump rows: one before level 0, one after D-1
+struct MfArgs {
+  int W, H, D, nmt, nt, z, tiles_x, ntiles, tiles_per_xcd;
+};
+// w0 = view | s << 16 | (delta < 0) << 24;  w1 = A row 0 pixel - x0 (xo);
+// w2 = B column 0 - x0 at nt = 0;  w3 = last row of the M-tile inside the tile
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+template <int K>
+__global__ __launch_bounds__(256) void k_ncc_mfma(const uint2* __restrict__ stats, const uint2* __restrict__ pk,
+                                                  const i32x4* __restrict__ mtiles, MfArgs a,
+                                                  float* __restrict__ vol) {
+  constexpr int R = K / 2, NK = K * K;
+  constexpr bool FPF = K == 5;
+  constexpr unsigned HI_MASK = ((1u << (8 * (K - 4))) - 1u);
+  extern __shared__ float lacc[];  // [D + 2 MF_LOFF][MF_PITCH]
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int W = a.W, H = a.H, D = a.D, NT = a.nt;
+  const int Hp2 = (H + 1) >> 1;
+  const long Pv = (long)W * Hp2 * 2;
+  const long P = (long)W * H;
+  const int bid = blockIdx.x, grp = bid & 7;
+  const int tile = grp * a.tiles_per_xcd + (bid >> 3);
+  if (tile >= a.ntiles) return;
+  const int x0 = (tile % a.tiles_x) * MF_X, y = tile / a.tiles_x;
+  const int x = x0 + lane;
+  const long zo = (long)a.z * Pv;
+  const uint2 rst = stats[zo + pair_index(y, min(x, W - 1), W)];
+  const float ivr = __int_as_float((int)rst.y);
+  const bool row_valid = y >= R && y + R < H;  // otherwise every window is invalid: cost 2
+
+  if (row_valid) {
+    for (int i = tid; i < D * MF_X; i += 256) lacc[(i / MF_X + MF_LOFF) * MF_PITCH + (i % MF_X)] = -INFINITY;
+    // K-group of this lane: the 16-byte slot (row pair) it reads and which of
+    // its two 8-byte rows belong to the window (the A mask zeroes the rest)
+    const int h = lane >> 4, g = h, jj = lane & 15;
+    const int first = y - R;
+    int slot;
+    unsigned m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;
+    if (h < R) {  // a full pair of window rows
+      slot = ((first + (first & 1)) >> 1) + h;
+      m0 = m2 = 0xffffffffu;
+      m1 = m3 = HI_MASK;
+    } else if (h == R) {  // the single remaining row: the last (first even) or the first (first odd)
+      if ((first & 1) == 0) {
+        slot = (y + R) >> 1;
+        m0 = 0xffffffffu; m1 = HI_MASK;
+      } else {
+        slot = first >> 1;
+        m2 = 0xffffffffu; m3 = HI_MASK;
+      }
+    } else {
+      slot = 0;
+    }
+    slot = min(max(slot, 0), Hp2 - 1);
+    const u32x4* pkrow = (const u32x4*)pk + (long)slot * W;  // + view * Pv/2 + column
+    const unsigned boff = (unsigned)slot * (unsigned)W * 16u;  // byte offset of this lane's slot row
+    const long st_row = (long)(y >> 1) * W * 2 + (y & 1);   // stats (uint2) index of (y, column 0)
+    const i32x4 batch = mtiles[min(wave + 4 * lane, a.nmt - 1)];
+    __syncthreads();
+
+    struct Bop {
+      i32x4 B;
+      uint2 sb;
+    };
+    const int nw = a.nmt > wave ? (a.nmt - wave + 3) >> 2 : 0;  // this wave's M-tiles (<= 64)
+    const uint2* rstats = stats + zo + st_row;
+    // M-tile k's reference operand and row sums, loaded one M-tile ahead
+    struct Mt {
+      int view, s, neg, xo, co0, imax;
+    };
+    auto decode = [&](int k) {
+      Mt m;
+      const int w0 = __builtin_amdgcn_readlane(batch.x, k);
+      m.view = w0 & 0xffff;
+      m.s = (w0 >> 16) & 0xff;
+      m.neg = (w0 >> 24) & 1;
+      m.xo = __builtin_amdgcn_readlane(batch.y, k);
+      m.co0 = __builtin_amdgcn_readlane(batch.z, k);
+      m.imax = __builtin_amdgcn_readlane(batch.w, k);
+      return m;
+    };
+    struct Mload {
+      u32x4 av;
+      int sv[4];
+    };
+    auto mload = [&](const Mt& m, Mload& o) {
+      // rows past the tile repeat its last pixel: their LDS maxima are
+      // duplicates, so partial M-tiles need no masking
+      o.av = pkrow[(zo >> 1) + min(x0 + m.xo + m.s * min(jj, m.imax), W - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; q++) o.sv[q] = (int)rstats[2 * min(x0 + m.xo + m.s * min(4 * g + q, m.imax), W - 1)].x;
+    };
+    Mload ml;
+    if (nw > 0) mload(decode(0), ml);
+    for (int k = 0; k < nw; k++) {
+      const Mt mt = decode(k);
+      const int view = mt.view, s = mt.s, neg = mt.neg, xo = mt.xo, co0 = mt.co0, imax = mt.imax;
+      const i32x4 A = i32x4{(int)(ml.av.x & m0), (int)(ml.av.y & m1), (int)(ml.av.z & m2), (int)(ml.av.w & m3)};
+      // this lane's output rows i = 4g + q: row sums and LDS addresses; level
+      // of (i, jj) at N-tile nt is D-1 + i - jj - 16 nt, or jj - i + 16 nt (delta < 0)
+      float nsr[4];
+      int aq[4], dq[4], cq[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int ic = min(4 * g + q, imax);  // a duplicate of row imax past the tile
+        cq[q] = xo + s * ic;
+        nsr[q] = FPF ? -__int_as_float(ml.sv[q]) : __int_as_float(-ml.sv[q]);
+        dq[q] = neg ? 4 * g - ic : ic - 4 * g;
+        aq[q] = (dq[q] + MF_LOFF) * MF_PITCH + cq[q];
+      }
+      if (k + 1 < nw) mload(decode(k + 1), ml);  // next M-tile's operands, in flight during this one
+      const int rbr = neg ? (jj - 4 * g) : (D - 1 + 4 * g - jj);  // level of (4g, jj) at nt = 0
+      const int rb = rbr * MF_PITCH;
+      const int rstep = neg ? 16 : -16;  // level step per N-tile
+      // N-tiles holding levels outside [0, D): the first and the last one or two
+      const int nt_hi_edge = max(1, min(NT, neg ? D / 16 : (D - 16) / 16 + 1));
+      // neighbour operand of N-tile nt: 32-bit byte offsets from wave-uniform bases
+      const char* bbase = (const char*)((const u32x4*)pk + (long)view * (Pv >> 1));
+      const char* sbase = (const char*)(stats + (long)view * Pv + st_row);
+      const int cb = x0 + co0 + s * jj, cstep = 16 * s;
+      auto loadb = [&](int nt, Bop& o) {
+        int c = cb + cstep * nt;
+        asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(c), "s"(W - 1));
+        const u32x4 bv = *(const u32x4*)(bbase + (boff + ((unsigned)c << 4)));
+        o.B = i32x4{(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
+        o.sb = *(const uint2*)(sbase + ((unsigned)c << 4));
+      };
+      // finish of two N-tiles, in lockstep across their 8 outputs (independent
+      // chains interleaved).  EDGE: N-tiles whose band cells may fall outside
+      // [0, D), clamped into the dump rows.
+      auto finish2 = [&](auto edge_tag, const i32x4& accA, const uint2& sbA, int ntA, const i32x4& accB,
+                         const uint2& sbB, int ntB) {
+        constexpr bool EDGE = decltype(edge_tag)::value;
+        float f[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          f[q] = (float)accA[q];
+          f[4 + q] = (float)accB[q];
+        }
+        if (FPF) {
+#pragma unroll
+          for (int q = 0; q < 8; q++) f[q] = (float)NK * f[q];
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            f[q] = __builtin_fmaf(nsr[q], __int_as_float((int)sbA.x), f[q]);
+            f[4 + q] = __builtin_fmaf(nsr[q], __int_as_float((int)sbB.x), f[4 + q]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            f[q] = (float)(__mul24(NK, accA[q]) + __mul24(__float_as_int(nsr[q]), (int)sbA.x));
+            f[4 + q] = (float)(__mul24(NK, accB[q]) + __mul24(__float_as_int(nsr[q]), (int)sbB.x));
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) f[q] = f[q] * fabsf(f[q]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          f[q] = f[q] * __int_as_float((int)sbA.y);
+          f[4 + q] = f[4 + q] * __int_as_float((int)sbB.y);
+        }
+        // an invalid neighbour window gives NaN: ds_max_f32 keeps the stored
+        // value then (IEEE maxNum, as v_max_f32; pinned by the border cells of
+        // the parity tests)
+        int ad[8];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int nt = u ? ntB : ntA;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            if (EDGE) {
+              int row = rbr + rstep * nt + dq[q];
+              asm("v_med3_i32 %0, %1, -1, %2" : "=v"(row) : "v"(row), "s"(D));
+              ad[4 * u + q] = (row + MF_LOFF) * MF_PITCH + cq[q];
+            } else {
+              ad[4 * u + q] = rb + rstep * MF_PITCH * nt + aq[q];
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          __hip_atomic_fetch_max(lacc + ad[q], f[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      // N-tiles 0 .. NT-1, two per step: both products issued before either
+      // finish, the next pair's operands loaded into the other register pair
+      // (4 operand sets, so no load lands in a register still in use); an odd
+      // count repeats the last N-tile, which the maximum absorbs
+      auto pair = [&](const Bop& x0p, const Bop& x1p, Bop& y0p, Bop& y1p, int nt) {
+        const int nt1 = min(nt + 1, NT - 1);
+        const i32x4 acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, x0p.B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, x1p.B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        loadb(min(nt + 2, NT - 1), y0p);
+        loadb(min(nt + 3, NT - 1), y1p);
+        if (nt == 0 || nt1 >= nt_hi_edge)
+          finish2(std::true_type{}, acc0, x0p.sb, nt, acc1, x1p.sb, nt1);
+        else
+          finish2(std::false_type{}, acc0, x0p.sb, nt, acc1, x1p.sb, nt1);
+        // keep the next pair's products below these finishes: hoisted, they
+        // would wait on the loads just issued
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      Bop b0, b1, b2, b3;
+      loadb(0, b0);
+      loadb(min(1, NT - 1), b1);
+      int nt = 0;
+      for (; nt + 2 < NT; nt += 4) {
+        pair(b0, b1, b2, b3, nt);
+        pair(b2, b3, b0, b1, nt + 2);
+      }
+      if (nt < NT) pair(b0, b1, b2, b3, nt);
+    }
+    __syncthreads();
+  }
+  // cost = 1 - max(-1, m ivr) per level, 64-column coalesced rows
+  if (x >= W) return;
+  float* vy = vol + (long)y * W + x;
+  const float ivr_e = row_valid ? ivr : __int_as_float(0x7fc00000);
+  int l = wave;
+  for (; l + 12 < D; l += 16) {
+    float m[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) m[u] = row_valid ? lacc[(l + 4 * u + MF_LOFF) * MF_PITCH + lane] : -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 4; u++) vy[(long)(l + 4 * u) * P] = 1.0f - vmax(m[u] * ivr_e, -1.0f);
+  }
+  for (; l < D; l += 4) {
+    const float m = row_valid ? lacc[(l + MF_LOFF) * MF_PITCH + lane] : -INFINITY;
+    vy[(long)l * P] = 1.0f - vmax(m * ivr_e, -1.0f);
+  }
+}
+
+// M-tile table + launch; returns 1 when the neighbour set is not eligible.
+template <int K>
+int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, int W, int H, int D, int z, int nn,
+                    const int* view, const float* levels, const float* fdx, const float* fdy, float bl,
+                    float* vol) {
+  std::vector<int32_t> tab;
+  for (int n = 0; n < nn; n++) {
+    const int t0 = (int)roundf(levels[0] * fdx[n]);
+    const int delta = D > 1 ? (int)roundf(levels[1] * fdx[n]) - t0 : 1;
+    if (delta == 0 || view[n] > 0xffff) return 1;
+    for (int l = 0; l < D; l++)
+      if ((int)roundf(levels[l] * fdx[n]) != t0 + l * delta || (int)roundf((bl * levels[l]) * fdy[n]) != 0) return 1;
+    const int s = delta < 0 ? -delta : delta;
+    if (s > 16) return 1;  // wider strides leave most MFMA rows idle
+    const int J0 = delta > 0 ? D - 1 : 0;
+    for (int rho = 0; rho < s; rho++) {
+      const int cnt = (MF_X - rho + s - 1) / s;  // pixels of the residue class in the tile
+      for (int m = 0; 16 * m < cnt; m++) {
+        const int xo = rho + 16 * s * m;
+        const int32_t e[4] = {view[n] | (s << 16) | (delta < 0 ? 1 << 24 : 0), xo, xo - t0 - s * J0,
+                              std::min(15, cnt - 16 * m - 1)};
+        tab.insert(tab.end(), e, e + 4);
+      }
+    }
+  }
+  const int nmt = (int)(tab.size() / 4);
+  if (nmt > 256) return 1;  // one 64-record batch per wave
+  int rc = 0;
+  const i32x4* dev = (const i32x4*)plan_upload(ctx, tab, &rc);
+  if (rc) return rc;
+  MfArgs a{};
+  a.W = W; a.H = H; a.D = D; a.z = z;
+  a.nmt = nmt;
+  a.nt = (D + 15 + 15) / 16;  // N-tiles covering the band j - i in [0, D-1]
+  a.tiles_x = (W + MF_X - 1) / MF_X;
+  a.ntiles = a.tiles_x * H;
+  a.tiles_per_xcd = (a.ntiles + 7) / 8;
+  const size_t lds = sizeof(float) * (size_t)(D + 2 * MF_LOFF) * MF_PITCH;
+  if (lds > 160 * 1024) return 1;
+  auto kern = k_ncc_mfma<K>;
+  if (lds > 64 * 1024)
+    MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            "hipFuncSetAttribute(ncc mfma lds)");
+  hipLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(256), lds, ctx->stream, stats, pk, dev, a, vol);
+  MVS_LAUNCH_CHECK("k_ncc_mfma");
+  return 0;
 }
 
 // Host side: the chunk/level shift plan (every roundf of the definition is
@@ -490,6 +796,16 @@ int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, con
   }
   const uint2* stats = (const uint2*)box;
   const uint2* pk = stats + (long)V * W * (H + (H & 1));
+  // MVS_NCC_MFMA=1: the matrix-core sweep for horizontal arrays with integer
+  // level steps (bit-identical; measured slower than the vector sweep on
+  // MI355X), else the vector sweep
+  const char* mf = getenv("MVS_NCC_MFMA");
+  if (mf && mf[0] == '1' && a.nn > 0) {
+    const int rc = K == 5 ? launch_ncc_mfma<5>(ctx, stats, pk, W, H, D, z, a.nn, a.view, levels_host, fdx, fdy, bl, vol)
+                 : K == 7 ? launch_ncc_mfma<7>(ctx, stats, pk, W, H, D, z, a.nn, a.view, levels_host, fdx, fdy, bl, vol)
+                          : 1;
+    if (rc != 1) return rc;
+  }
   // tile height and levels per wave: MVS_NCC_TH (8|16), MVS_NCC_DPW (1|2|4)
   static const int dpw_env = [] {
     const char* e = getenv("MVS_NCC_DPW");

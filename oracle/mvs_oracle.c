@@ -336,9 +336,12 @@ void orc_sweep(int V, int W, int H, int S, const float* lab, float* spixl, const
 /*   reference and the shifted window lies inside the image.                */
 /*   num = n*Srp - Sr*Sp, vr = n*Srr - Sr^2, vp = n*Spp - Sp^2 (int32);     */
 /*   ivr = vr ? 1/(float)vr : 0, ivp likewise (per pixel, IEEE);            */
-/*   e = ((a*|a|)*ivr)*ivp with a = (float)num: the signed squared NCC (0   */
-/*   on textureless windows); E = max(-1, max over VALID neighbours of e);  */
-/*   vol[d][y][x] = 1 - E  (2 when no neighbour window is valid).           */
+/*   e = (a*|a|)*ivp with a = (float)num; m = max over VALID neighbours  */
+/*   of e (-inf if none); E = m*ivr: the best signed squared NCC (0 on a    */
+/*   textureless reference window; NaN when m = -inf and ivr = 0);          */
+/*   vol[d][y][x] = 1 - max(-1, E)  (2 when no neighbour window is valid;   */
+/*   max(-1, NaN) = -1).  ivr is applied after the maximum: rounding is     */
+/*   monotone, so this equals the maximum of the per-neighbour products.    */
 /* ------------------------------------------------------------------------ */
 void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, int D, const int* vs,
                     const int* sn, int aw, float bl, int K, int z, float* vol) {
@@ -360,7 +363,7 @@ void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, 
       int vr = nk * Srr - Sr * Sr;
       for (int dl = 0; dl < D; dl++) {
         float d = levels[dl];
-        float best = -1.0f;
+        float best = -INFINITY;
         for (int n = 0; n < sn[z]; n++) {
           int view = vs[V * z + n];
           int dx = view % aw - rx, dy = view / aw - ry;
@@ -378,15 +381,16 @@ void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, 
             }
           int vp = nk * Spp - Sp * Sp;
           int num = nk * Srp - Sr * Sp;
-          float ivr = vr != 0 ? 1.0f / (float)vr : 0.0f;
           float ivp = vp != 0 ? 1.0f / (float)vp : 0.0f;
           float a = (float)num;
           float e = a * fabsf(a);
-          e = e * ivr;
           e = e * ivp;
           if (e > best) best = e;
         }
-        vol[((long)dl * H + y) * W + x] = 1.0f - best;
+        float ivr = vr != 0 ? 1.0f / (float)vr : 0.0f;
+        float E = best * ivr;
+        if (!(E > -1.0f)) E = -1.0f;
+        vol[((long)dl * H + y) * W + x] = 1.0f - E;
       }
     }
 }

@@ -56,6 +56,7 @@ def main():
         out["sweep_spixl_5views"] = timeit(lambda: e.sweep_spixl(lab, sp, rep, cam, 32))
     if run("ncc"):
         out["ncc_volume_1view"] = timeit(lambda: e.ncc_volume(l8, box, cam, 2, 5, out=vol))
+        out["ncc_volume_view0"] = timeit(lambda: e.ncc_volume(l8, box, cam, 0, 5, out=vol))
     if run("wta"):
         out["wta_1view"] = timeit(lambda: e.wta(vol, lv))
     if run("sad"):

@@ -25,7 +25,7 @@ PIXEL_CASES = {
 def build(c: dict):
     V = c["aw"] * c["ah"]
     stack, gt = synth.make_stack(c["W"], c["H"], c["aw"], c["ah"], c["dmin"], c["dmax"], c["bl"], c["seed"])
-    levels = params.disparity_levels(c["dmin"], c["dmax"], 1)
+    levels = params.disparity_levels(c["dmin"], c["dmax"], c.get("inc", 1))
     vs, sn = params.flatten_subsets(params.neighbour_lists(c["aw"], c["ah"], c["nh"], c["nv"]))
     return dict(V=V, stack=stack, gt=gt, levels=levels, vs=vs, sn=sn)
 

@@ -229,7 +229,7 @@ def _box(a, r):
 
 def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
     """Build-defined NCC K x K cost volume (csrc/ncc.hip header) -> [D][H][W]:
-    1 - max(-1, max over valid neighbour windows of the signed squared NCC)."""
+    1 - max(-1, ivr * max over valid neighbour windows of (a|a|) ivp)."""
     V, H, W = q.shape
     r, nk = K // 2, K * K
     bl = f32(bl)
@@ -245,7 +245,7 @@ def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
     rin = (x - r >= 0) & (x + r < W) & (y - r >= 0) & (y + r < H)
     vol = np.zeros((len(levels), H, W), f32)
     for dl, d in enumerate(np.asarray(levels, f32)):
-        best = np.full((H, W), f32(-1), f32)
+        best = np.full((H, W), -np.inf, f32)
         for n in range(sn[z]):
             view = vs[z, n]
             dx, dy = view % aw - rx, view // aw - ry
@@ -269,10 +269,11 @@ def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
             vp = nk * Spp - Sp * Sp
             ivp = np.where(vp != 0, f32(1) / np.where(vp != 0, vp, 1).astype(f32), f32(0)).astype(f32)
             a = (nk * Srp - Sr * Sp).astype(f32)
-            e = (a * np.abs(a)) * ivr
-            e = e * ivp
+            e = (a * np.abs(a)) * ivp
             best = np.where(ok & (e > best), e, best).astype(f32)
-        vol[dl] = f32(1) - best
+        with np.errstate(invalid="ignore"):
+            E = (best * ivr).astype(f32)  # -inf * 0 = NaN: no valid window
+        vol[dl] = f32(1) - np.where(E > f32(-1), E, f32(-1)).astype(f32)
     return vol
 
 

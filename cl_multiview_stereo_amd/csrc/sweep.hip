@@ -13,6 +13,8 @@
 //  (the NCC cost-volume kernels are in ncc.hip)
 //  k_wta             winner-take-all + confidence over the materialised volume
 //                    (the HBM-streaming pass the roofline is quoted on).
+#include <cstdlib>
+
 #include "mvs_internal.h"
 
 namespace mvs {
@@ -269,38 +271,11 @@ __global__ __launch_bounds__(256) void k_sweep_pixel_sad(const float4* __restric
 }
 
 // ---- winner-take-all + confidence ----------------------------------------
-__global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, const float* __restrict__ levels, long P,
-                                             int D, float* __restrict__ disp, float* __restrict__ conf) {
-  long p = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  // 4 smallest (cost, index) in lexicographic order
+// the 4 smallest (cost, level) of one pixel in lexicographic order
+struct Top4 {
   float v0 = 1000000.0f, v1 = 1000000.0f, v2 = 1000000.0f, v3 = 1000000.0f;
   int i0 = -1, i1 = -1, i2 = -1, i3 = -1;
-  const float* col = vol + p;
-  int dl = 0;
-  for (; dl + 4 <= D; dl += 4) {
-    float c[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) c[u] = __builtin_nontemporal_load(col + (long)(dl + u) * P);
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      float cc = c[u];
-      int ci = dl + u;
-      if (cc < v3) {
-        if (cc < v2) {
-          v3 = v2; i3 = i2;
-          if (cc < v1) {
-            v2 = v1; i2 = i1;
-            if (cc < v0) { v1 = v0; i1 = i0; v0 = cc; i0 = ci; }
-            else { v1 = cc; i1 = ci; }
-          } else { v2 = cc; i2 = ci; }
-        } else { v3 = cc; i3 = ci; }
-      }
-    }
-  }
-  for (; dl < D; dl++) {
-    float cc = col[(long)dl * P];
-    int ci = dl;
+  __device__ __forceinline__ void insert(float cc, int ci) {
     if (cc < v3) {
       if (cc < v2) {
         v3 = v2; i3 = i2;
@@ -312,14 +287,46 @@ __global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, cons
       } else { v3 = cc; i3 = ci; }
     }
   }
-  disp[p] = i0 >= 0 ? levels[i0] : 0.0f;
-  if (conf) {
-    float c2 = 1000000.0f;
-    if (i1 >= 0 && (i1 < i0 - 1 || i1 > i0 + 1)) c2 = v1;
-    else if (i2 >= 0 && (i2 < i0 - 1 || i2 > i0 + 1)) c2 = v2;
-    else if (i3 >= 0 && (i3 < i0 - 1 || i3 > i0 + 1)) c2 = v3;
-    conf[p] = (i0 < 0 || c2 == 1000000.0f) ? 0.0f : c2 - v0;
+  __device__ __forceinline__ void emit(const float* levels, float* disp, float* conf, long p) const {
+    disp[p] = i0 >= 0 ? levels[i0] : 0.0f;
+    if (conf) {
+      float c2 = 1000000.0f;
+      if (i1 >= 0 && (i1 < i0 - 1 || i1 > i0 + 1)) c2 = v1;
+      else if (i2 >= 0 && (i2 < i0 - 1 || i2 > i0 + 1)) c2 = v2;
+      else if (i3 >= 0 && (i3 < i0 - 1 || i3 > i0 + 1)) c2 = v3;
+      conf[p] = (i0 < 0 || c2 == 1000000.0f) ? 0.0f : c2 - v0;
+    }
   }
+};
+
+// One lane per NP consecutive pixels (NP-wide non-temporal vector loads, so a
+// wave streams 256 NP contiguous bytes per level), UNR levels in flight.
+template <int NP, int UNR>
+__global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, const float* __restrict__ levels, long P,
+                                             int D, float* __restrict__ disp, float* __restrict__ conf) {
+  typedef float vec __attribute__((ext_vector_type(NP)));
+  const long p = (blockIdx.x * (long)blockDim.x + threadIdx.x) * NP;
+  if (p >= P) return;
+  Top4 t[NP];
+  const vec* col = (const vec*)(vol + p);
+  const long Pv = P / NP;
+  int dl = 0;
+  for (; dl + UNR <= D; dl += UNR) {
+    vec c[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) c[u] = __builtin_nontemporal_load(col + (long)(dl + u) * Pv);
+#pragma unroll
+    for (int u = 0; u < UNR; u++)
+#pragma unroll
+      for (int k = 0; k < NP; k++) t[k].insert(c[u][k], dl + u);
+  }
+  for (; dl < D; dl++) {
+    const vec c = col[(long)dl * Pv];
+#pragma unroll
+    for (int k = 0; k < NP; k++) t[k].insert(c[k], dl);
+  }
+#pragma unroll
+  for (int k = 0; k < NP; k++) t[k].emit(levels, disp, conf, p + k);
 }
 
 }  // namespace
@@ -366,7 +373,9 @@ int launch_sweep_pixel_sad(hipStream_t s, int V, int W, int H, const float* lab,
 int launch_wta(hipStream_t s, int W, int H, int D, const float* vol, const float* levels, float* disp,
                float* conf) {
   long P = (long)W * H;
-  hipLaunchKernelGGL(k_wta, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, vol, levels, P, D, disp, conf);
+  // one pixel per lane, 8 levels in flight (wider per-lane vectors measured no faster)
+  hipLaunchKernelGGL((k_wta<1, 8>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, vol, levels, P, D, disp,
+                     conf);
   MVS_LAUNCH_CHECK("k_wta");
   return 0;
 }

@@ -170,6 +170,7 @@ class EngineBackend:
 
     def __init__(self, engine):
         self.e = engine
+        self._sweeps = {}  # PixelSweep (volume buffers, side stream) per configuration
 
     def cvt(self, rgbx):
         return self.e.cvt(rgbx, want_l8=True)
@@ -188,7 +189,11 @@ class EngineBackend:
     def pixel_sweep(self, lab, l8, cam, z0, z1, cost, K):
         from .pipeline import PixelSweep
         H, W = lab.shape[1:3]
-        return PixelSweep(self.e, cam, W, H, cost, K).run(lab, l8, z0, z1)
+        key = (id(cam), W, H, cost, K)
+        ps = self._sweeps.get(key)
+        if ps is None:
+            ps = self._sweeps[key] = PixelSweep(self.e, cam, W, H, cost, K)
+        return ps.run(lab, l8, z0, z1)
 
     def flatness(self, spixl, gamma):
         return self.e.flatness(spixl, gamma)

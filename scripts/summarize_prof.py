@@ -59,15 +59,16 @@ def main():
             v["hbm_read_bytes_corrected"] = 2.0 * v["FETCH_SIZE_bytes_per_launch"]
         v["hbm_bytes_per_launch"] = v.get("hbm_read_bytes_corrected", 0.0) + v.get("WRITE_SIZE_bytes_per_launch", 0.0)
     json.dump(pmc, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
-    if "k_wta" in pmc:
-        json.dump({"kernel": "k_wta", "source": f"profiles/{tag}_pmc.json",
-                   "hbm_bytes_per_launch": pmc["k_wta"]["hbm_bytes_per_launch"],
+    wta = next((k for k in sorted(pmc) if k.startswith("k_wta")), None)
+    if wta:
+        json.dump({"kernel": wta, "source": f"profiles/{tag}_pmc.json",
+                   "hbm_bytes_per_launch": pmc[wta]["hbm_bytes_per_launch"],
                    "note": "2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes"},
                   open(os.path.join(out, "pmc_wta.json"), "w"), indent=1)
     for r in rows[:8]:
         print(f"{short(r[0]):40s} calls={r[1]:5d} avg={r[3]:9.3f} us  {r[4]:6.2f}%")
-    for k in ("k_wta", "k_ncc_volume<5, 16>", "k_cvt", "k_update", "k_assign"):
-        if k in pmc:
+    for k in sorted(pmc):
+        if k.split("<")[0] in ("k_wta", "k_ncc_volume", "k_cvt", "k_update_tiles", "k_assign", "k_box_stats"):
             print(k, {a: round(b / 1e6, 2) for a, b in pmc[k].items() if "bytes" in a})
 
 

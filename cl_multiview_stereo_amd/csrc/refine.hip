@@ -226,40 +226,65 @@ __device__ float comp_smoothness(const PCtx& p, float d, float nx, float ny, flo
   return wn > 0 ? sm / wn : 0.000001f;
 }
 
+// compute_consistency (clcode.cl:1471-1565).  The candidate plane's disparity
+// at the 9 sample points does not depend on the view: evaluated once.  Per
+// view, all 9 label gathers are issued before the record gathers that depend
+// on them, and the accumulation is branch-free (a sample outside the image
+// leaves every sum unchanged), so the gathers overlap instead of forming 9
+// round trips.  A label is the superpixel index y*mw + x, so the record is at
+// view * M + label (the reference's % and / recombine to it exactly).
 __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, float nz) {
   const RArgs& c = p.c;
-  long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
+  const long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
   float cons = 0.0f;
   int vc = 0;
-  int camx = p.z % c.aw, camy = p.z / c.aw;
+  const int camx = p.z % c.aw, camy = p.z / c.aw;
+  const int cxi = (int)p.cx, cyi = (int)p.cy;
+  float sxf[9], syf[9], di[9];
+#pragma unroll
+  for (int s = 0; s < 9; s++) {  // (i, j) = (s / 3 - 1, s % 3 - 1): i outer, j inner
+    sxf[s] = (float)(cxi + p.smp[s] * (s / 3 - 1));
+    syf[s] = (float)(cyi + p.smp[s] * (s % 3 - 1));
+    di[s] = plane_at(nx, ny, nz, p.cx, p.cy, d, sxf[s], syf[s]);
+  }
   for (int k = 0; k < p.sn[p.z]; k++) {
-    int view = p.vs[c.V * p.z + k];
+    const int view = p.vs[c.V * p.z + k];
+    const float fdx = (float)(view % c.aw - camx), fdy = (float)(view / c.aw - camy);
+    const uint32_t* lv = p.labels + P * view;
+    int xp[9], yp[9];
+    bool ok[9];
+    uint32_t ip[9];
+#pragma unroll
+    for (int s = 0; s < 9; s++) {
+      xp[s] = (int)(sxf[s] - roundf(di[s] * fdx));
+      yp[s] = (int)(syf[s] - roundf((c.bl * di[s]) * fdy));
+      ok[s] = xp[s] >= 0 && yp[s] >= 0 && xp[s] < c.W && yp[s] < c.H;
+      ip[s] = lv[ok[s] ? (long)c.W * yp[s] + xp[s] : 0];
+    }
     float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
-    int vx = view % c.aw, vy = view / c.aw;
-    for (int i = -1; i <= 1; i++)
-      for (int j = -1; j <= 1; j++) {
-        int sx = (int)p.cx + p.smp[(i + 1) * 3 + j + 1] * i;
-        int sy = (int)p.cy + p.smp[(i + 1) * 3 + j + 1] * j;
-        float di = plane_at(nx, ny, nz, p.cx, p.cy, d, (float)sx, (float)sy);
-        int xp = (int)((float)sx - roundf(di * (float)(vx - camx)));
-        int yp = (int)((float)sy - roundf((c.bl * di) * (float)(vy - camy)));
-        if (xp >= 0 && yp >= 0 && xp < c.W && yp < c.H) {
-          uint32_t ip = p.labels[P * view + (long)c.W * yp + xp];
-          uint32_t qx = ip % (uint32_t)c.mw, qy = ip / (uint32_t)c.mw;
-          long q = M * view + (long)c.mw * qy + qx;
-          const float* s = p.spixl + 8 * q;
-          const float* sq = p.st + 6 * q;
-          float dip = plane_at(sq[3], sq[4], sq[5], s[1], s[2], sq[0], (float)xp, (float)yp);
-          float diff = dip - di;
-          float wv = fabsf(diff) < c.fuse ? 1.0f : 0.0f;
-          visible = visible + wv * expf_neg_sq(diff, c.alpha);
-          vis_w = vis_w + wv;
-          occ_w = occ_w + (1.0f - wv);
-          diff = mvs_distance3(s[3], s[4], s[5], p.col[0], p.col[1], p.col[2]);
-          visibility = visibility + expf_neg_sq(diff, c.gamma);
-          num = num + 1.0f;
-        }
+#pragma unroll
+    for (int s = 0; s < 9; s++) {
+      const long q = M * view + ip[s];
+      const float4 sa = *(const float4*)(p.spixl + 8 * q);      // s0..s3
+      const float2 sb = *(const float2*)(p.spixl + 8 * q + 4);  // s4, s5
+      const float* sq = p.st + 6 * q;
+      const float2 t0 = *(const float2*)(sq);      // sq0 (d)
+      const float2 t1 = *(const float2*)(sq + 2);  // sq3 (nx)
+      const float2 t2 = *(const float2*)(sq + 4);  // sq4, sq5 (ny, nz)
+      float dip = plane_at(t1.y, t2.x, t2.y, sa.y, sa.z, t0.x, (float)xp[s], (float)yp[s]);
+      float diff = dip - di[s];
+      const float wv = fabsf(diff) < c.fuse ? 1.0f : 0.0f;
+      const float t_vis = wv * expf_neg_sq(diff, c.alpha);
+      diff = mvs_distance3(sa.w, sb.x, sb.y, p.col[0], p.col[1], p.col[2]);
+      const float t_col = expf_neg_sq(diff, c.gamma);
+      if (ok[s]) {
+        visible = visible + t_vis;
+        vis_w = vis_w + wv;
+        occ_w = occ_w + (1.0f - wv);
+        visibility = visibility + t_col;
+        num = num + 1.0f;
       }
+    }
     if (num > 0) {
       vc++;
       if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);

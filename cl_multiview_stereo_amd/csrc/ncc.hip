@@ -111,15 +111,15 @@ struct NccArgs {
   int view[kMaxNbr];
   int pk_pairs, st_pairs;  // LDS band heights in row pairs; the pair-row stride is the template BW
 };
-// host-built plan (device memory, cached per context): one 64-B record per
+// host-built plan (device memory, cached per context): one 128-B record per
 // (chunk c, neighbour n, wave w), read with one scalar load per neighbour.
 // A __restrict__ kernel parameter, so the loads are SMEM and never wait on
 // the vector-memory counter the LDS-DMA prefetch runs under.
-struct alignas(64) NccRec {
+struct alignas(128) NccRec {
   int txmax, tymax;  // band origin: image column x0 - txmax; pk pair (y0-R-tymax)>>1, stats pair (y0-tymax)>>1
   int bhp, shp;      // pk pair rows to stage, stats pair rows | (64-px blocks per row) << 16
-  int lv[8];         // per level j of wave w: {txmax - tx, pk start row | stats start row << 16 (band-relative)}
-  int pad[4];
+  int lv[16];        // per level j of wave w: {txmax - tx, pk start row | stats start row << 16 (band-relative)}
+  int pad[12];
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -679,7 +679,7 @@ inline int floor_half(int v) { return v >> 1; }  // arithmetic: floor(v / 2)
 template <int K, int TH, int DPW>
 NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl) {
   constexpr int R = K / 2, NR = TH + 2 * R, DC = 4 * DPW;
-  static_assert(DPW <= 4, "NccRec holds 4 levels per wave");
+  static_assert(DPW <= 8, "NccRec holds 8 levels per wave");
   constexpr int RW = sizeof(NccRec) / 4;
   const int nch = (D + DC - 1) / DC;
   NccPlan p;
@@ -828,6 +828,7 @@ int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, con
       if (dpw_env >= 4) MVS_NCC_TRY(5, 16, 4)
       if (dpw_env >= 2) MVS_NCC_TRY(5, 16, 2)
     }
+    if (dpw_env >= 8) MVS_NCC_TRY(5, 8, 8)
     if (dpw_env >= 4) MVS_NCC_TRY(5, 8, 4)
     if (dpw_env >= 2) MVS_NCC_TRY(5, 8, 2)
     MVS_NCC_TRY(5, 8, 1)

@@ -543,6 +543,66 @@ __global__ void k_remove_incons(const float* __restrict__ proj, const float* __r
   out[P * r + p] = dest;
 }
 
+// The same output by candidate selection.  A candidate's stability depends
+// only on its disparity d (and the pixel and reference view), and the
+// reference keeps the largest d != 0 whose stability is >= 0 (its
+// `dest == 0 || dest < d` update).  So the candidates are tried from the
+// largest d down, every view holding that d retired together, and the first
+// stable one is the answer: usually one or two stability evaluations per
+// pixel instead of V, i.e. O(V) instead of O(V^2) work at V = 32 (C4).
+template <int MAXV>
+__global__ __launch_bounds__(256) void k_remove_incons_sel(const float* __restrict__ proj, const float* __restrict__ full,
+                                                           int V, int W, int H, int aw, float bl, float fuse, int z0,
+                                                           float* __restrict__ out) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
+  if (x >= W) return;
+  long P = (long)W * H, p = (long)y * W + x;
+  int crx = r % aw, cry = r / aw;
+  float pv[MAXV];
+  unsigned long long live = 0ull;  // candidates not yet tried: d != 0
+#pragma unroll
+  for (int i = 0; i < MAXV; i++) {
+    pv[i] = i < V ? proj[P * i + p] : 0.0f;
+    if (pv[i] != 0) live |= 1ull << i;
+  }
+  float dest = 0.0f;
+  while (live) {
+    float d = 0.0f;
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < MAXV; i++)
+      if (((live >> i) & 1ull) && (!any || pv[i] > d)) { d = pv[i]; any = true; }
+#pragma unroll
+    for (int i = 0; i < MAXV; i++)
+      if (pv[i] == d) live &= ~(1ull << i);
+    float stab = 0.0f;
+#pragma unroll
+    for (int j = 0; j < MAXV; j++) {
+      if (j < V && pv[j] != 0) {
+        const float diff = pv[j] - d;
+        if (fabsf(diff) > fuse) stab = stab - 1.0f;
+        if (fabsf(diff) <= fuse) stab = stab + 1.0f;
+      }
+    }
+    for (int j = 0; j < V; j++) {
+      int cx = j % aw, cy = j / aw;
+      int xx = (int)((float)x - roundf(d * (float)(cx - crx)));
+      int yy = (int)((float)y - roundf((bl * d) * (float)(cy - cry)));
+      if (xx >= 0 && yy >= 0 && xx < W && yy < H) {
+        float dc = full[P * j + (long)W * yy + xx];
+        float diff = dc - d;
+        if (fabsf(diff) > fuse) stab = stab - 1.0f;
+        if (fabsf(diff) < fuse) stab = stab + 1.0f;
+      }
+    }
+    if (stab >= 0) {
+      dest = d;
+      break;
+    }
+  }
+  out[P * r + p] = dest;
+}
+
 }  // namespace
 
 int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
@@ -588,8 +648,15 @@ int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fu
   hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, H, V), dim3(256), 0, s, full, V, W, H, aw, bl, proj);
   MVS_LAUNCH_CHECK("k_proj_inv");
   if (z1 > z0) {
-    hipLaunchKernelGGL(k_remove_incons, dim3((W + 255) / 256, H, z1 - z0), dim3(256), 0, s, proj, full, V, W, H,
-                       aw, bl, fuse, z0, out);
+    const dim3 g((W + 255) / 256, H, z1 - z0);
+    if (V <= 8)
+      hipLaunchKernelGGL(k_remove_incons_sel<8>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
+    else if (V <= 32)
+      hipLaunchKernelGGL(k_remove_incons_sel<32>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
+    else if (V <= 64)
+      hipLaunchKernelGGL(k_remove_incons_sel<64>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
+    else
+      hipLaunchKernelGGL(k_remove_incons, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
     MVS_LAUNCH_CHECK("k_remove_incons");
   }
   return 0;

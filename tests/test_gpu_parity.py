@@ -201,6 +201,22 @@ def test_filter(engine, name):
     assert_bits(out.cpu().numpy(), oout, "filter output")
 
 
+@pytest.mark.parametrize("aw,ah", [(8, 4), (9, 5), (10, 7)])
+def test_filter_many_views(engine, aw, ah):
+    # V = 32 / 45 / 70: the candidate-selection kernel at MAXV 32 and 64, and
+    # the direct kernel past 64 views; smooth disparities with ties, zeros and
+    # out-of-image projections
+    V, H, W = aw * ah, 24, 40
+    rng = np.random.default_rng(aw * 10 + ah)
+    base = rng.integers(2, 9, size=(V, 1, 1)).astype(np.float32)
+    disp = base + rng.choice(np.float32([0.0, 0.5, 1.0, 3.0]), size=(V, H, W))
+    disp[rng.random(disp.shape) < 0.1] = 0.0
+    proj, out = engine.filter(dev(disp), aw, 1.0, 1.0)
+    oproj, oout = orc.filt(disp, aw, 1.0, 1.0)
+    assert_bits(proj.cpu().numpy(), oproj, "filter projection")
+    assert_bits(out.cpu().numpy(), oout, "filter output")
+
+
 def test_determinism(engine):
     c = CASES["c5x1_s32"]
     b = build(c)

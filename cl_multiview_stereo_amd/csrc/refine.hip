@@ -584,7 +584,9 @@ __global__ __launch_bounds__(256) void k_remove_incons_sel(const float* __restri
         if (fabsf(diff) <= fuse) stab = stab + 1.0f;
       }
     }
-    for (int j = 0; j < V; j++) {
+    // each remaining view adds at most +1: stop once stab >= 0 is out of reach
+    // (stab counts exactly, so this only skips work)
+    for (int j = 0; j < V && stab + (float)(V - j) >= 0.0f; j++) {
       int cx = j % aw, cy = j / aw;
       int xx = (int)((float)x - roundf(d * (float)(cx - crx)));
       int yy = (int)((float)y - roundf((bl * d) * (float)(cy - cry)));

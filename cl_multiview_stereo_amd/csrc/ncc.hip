@@ -748,10 +748,10 @@ int launch_ncc_bw(hipStream_t s, const uint2* stats, const uint2* pk, const NccR
 // returns 1 if this variant does not fit the LDS (caller tries a smaller one)
 template <int K, int TH, int DPW>
 int launch_ncc_t(mvs_ctx* ctx, const uint2* stats, const uint2* pk, NccArgs& a, const float* levels_host,
-                 const float* fdx, const float* fdy, float bl, float* vol) {
+                 const float* fdx, const float* fdy, float bl, float* vol, size_t lds_cap) {
   NccPlan p = make_plan<K, TH, DPW>(levels_host, a.D, a.nn, fdx, fdy, bl);
   const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * p.band_w;
-  if (lds > 160 * 1024 || p.band_w > 256) return 1;
+  if (lds > lds_cap || p.band_w > 256) return 1;
   int rc = 0;
   const int32_t* dev = plan_upload(ctx, p.table, &rc);
   if (rc) return rc;
@@ -821,27 +821,32 @@ int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, con
     return e ? atoi(e) : 8;
   }();
   int rc = 1;
+  // first the widest variant whose double-buffered bands leave room for two
+  // workgroups per CU (vertical shifts grow the bands: fewer levels per step
+  // then beat a single resident workgroup), then any that fits the LDS
 #define MVS_NCC_TRY(KK, TT, PP)                                                                     \
-  if (rc == 1) rc = launch_ncc_t<KK, TT, PP>(ctx, stats, pk, a, levels_host, fdx, fdy, bl, vol);
-  if (K == 5) {
-    if (th_env == 16) {
-      if (dpw_env >= 4) MVS_NCC_TRY(5, 16, 4)
-      if (dpw_env >= 2) MVS_NCC_TRY(5, 16, 2)
+  if (rc == 1) rc = launch_ncc_t<KK, TT, PP>(ctx, stats, pk, a, levels_host, fdx, fdy, bl, vol, cap);
+  for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
+    if (K == 5) {
+      if (th_env == 16) {
+        if (dpw_env >= 4) MVS_NCC_TRY(5, 16, 4)
+        if (dpw_env >= 2) MVS_NCC_TRY(5, 16, 2)
+      }
+      if (dpw_env >= 8) MVS_NCC_TRY(5, 8, 8)
+      if (dpw_env >= 4) MVS_NCC_TRY(5, 8, 4)
+      if (dpw_env >= 2) MVS_NCC_TRY(5, 8, 2)
+      MVS_NCC_TRY(5, 8, 1)
+    } else if (K == 7) {
+      if (th_env == 16) {
+        if (dpw_env >= 4) MVS_NCC_TRY(7, 16, 4)
+        if (dpw_env >= 2) MVS_NCC_TRY(7, 16, 2)
+      }
+      if (dpw_env >= 4) MVS_NCC_TRY(7, 8, 4)
+      if (dpw_env >= 2) MVS_NCC_TRY(7, 8, 2)
+      MVS_NCC_TRY(7, 8, 1)
+    } else {
+      return arg_fail("NCC window must be 5 or 7");
     }
-    if (dpw_env >= 8) MVS_NCC_TRY(5, 8, 8)
-    if (dpw_env >= 4) MVS_NCC_TRY(5, 8, 4)
-    if (dpw_env >= 2) MVS_NCC_TRY(5, 8, 2)
-    MVS_NCC_TRY(5, 8, 1)
-  } else if (K == 7) {
-    if (th_env == 16) {
-      if (dpw_env >= 4) MVS_NCC_TRY(7, 16, 4)
-      if (dpw_env >= 2) MVS_NCC_TRY(7, 16, 2)
-    }
-    if (dpw_env >= 4) MVS_NCC_TRY(7, 8, 4)
-    if (dpw_env >= 2) MVS_NCC_TRY(7, 8, 2)
-    MVS_NCC_TRY(7, 8, 1)
-  } else {
-    return arg_fail("NCC window must be 5 or 7");
   }
 #undef MVS_NCC_TRY
   if (rc == 1) return arg_fail("NCC sweep: neighbour shifts too large for the LDS band");

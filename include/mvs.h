@@ -117,13 +117,14 @@ int mvs_sweep_pixel_sad_d(mvs_ctx* ctx, int W, int H, const float* lab, const mv
 
 /* Build-defined per-pixel NCC KxK plane sweep (definition: csrc/ncc.hip).
  * box int32 [2][V][Hp][W][2] (Hp = H rounded up to even; 16 B/px), from
- * mvs_box_stats_d, rows stored pairwise interleaved (element (y, x) of a view
- * at uint2 index ((y>>1)*W + x)*2 + (y&1)): plane 0 per-pixel window
- * statistics {S = sum q, bits(1/(n*sum q^2 - S^2)) (0 if textureless, NaN if
- * the window leaves the image)}; plane 1 the packed intensities
- * q(x-R .. x-R+7) of each pixel's row (two little-endian dwords).
- * vol [D][H][W] float cost of reference view z = 1 - max(-1, best signed
- * squared NCC over valid neighbour windows); l8 is validated only. */
+ * mvs_box_stats_d, rows stored pairwise interleaved: plane 0 per row pair
+ * (2m, 2m+1) and column x the float4 {a(2m), a(2m+1), b(2m), b(2m+1)} with
+ * s = 1/sqrt(n*sum q^2 - (sum q)^2) (0 if textureless, NaN if the window
+ * leaves the image), a = n*s, b = (sum q - 128 n)*s; plane 1 the centred
+ * packed intensities q-128 of columns x-R .. x-R+7 of each pixel's row (two
+ * little-endian dwords at uint2 index ((y>>1)*W + x)*2 + (y&1)).
+ * vol [D][H][W] float cost of reference view z = 1 - max(-1, best NCC over
+ * valid neighbour windows); l8 is validated only. */
 int mvs_box_stats_d(mvs_ctx* ctx, const uint8_t* l8, int V, int W, int H, int K, int32_t* box);
 int mvs_ncc_volume_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
                      int K, int z, float* vol);

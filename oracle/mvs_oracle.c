@@ -331,18 +331,21 @@ void orc_sweep(int V, int W, int H, int S, const float* lab, float* spixl, const
 
 /* ------------------------------------------------------------------------ */
 /* Build-defined per-pixel NCC cost volume (no reference counterpart).      */
-/*   q = L8 intensity; window K x K (r = K/2); shift (tx, ty) =             */
-/*   (roundf(d*dx), roundf((bl*d)*dy)); window valid iff every tap of the   */
-/*   reference and the shifted window lies inside the image.                */
-/*   num = n*Srp - Sr*Sp, vr = n*Srr - Sr^2, vp = n*Spp - Sp^2 (int32);     */
-/*   ivr = vr ? 1/(float)vr : 0, ivp likewise (per pixel, IEEE);            */
-/*   e = (a*|a|)*ivp with a = (float)num; m = max over VALID neighbours  */
-/*   of e (-inf if none); E = m*ivr: the best signed squared NCC (0 on a    */
-/*   textureless reference window; NaN when m = -inf and ivr = 0);          */
-/*   vol[d][y][x] = 1 - max(-1, E)  (2 when no neighbour window is valid;   */
-/*   max(-1, NaN) = -1).  ivr is applied after the maximum: rounding is     */
-/*   monotone, so this equals the maximum of the per-neighbour products.    */
+/*   q = L8 intensity, q' = q - 128; window K x K (r = K/2), n = K*K;       */
+/*   shift (tx, ty) = (roundf(d*dx), roundf((bl*d)*dy)); window valid iff   */
+/*   every tap of the reference and the shifted window lies in the image.   */
+/*   Centred integer sums Sr', Sp', Srp' and v = n*Sqq - Sq^2 (var, int32); */
+/*   s = v ? 1/sqrtf((float)v) : 0 per window (IEEE sqrt and divide);       */
+/*   per neighbour pixel a = n*s, b = Sp'*s (float), per cell              */
+/*   x = fmaf(-(float)Sr', b, (float)Srp' * a)   (= NCC * sqrt(vr));        */
+/*   m = max over VALID neighbours of x (-inf if none); E = m * s_r;        */
+/*   vol[d][y][x] = 1 - max(-1, E): 1 minus the best NCC, 1 on a textureless*/
+/*   reference window, 2 when no neighbour window is valid (-inf*0 = NaN,   */
+/*   max(-1, NaN) = -1).  s_r is applied after the maximum (rounding is     */
+/*   monotone, so this equals the maximum of the per-neighbour products).   */
 /* ------------------------------------------------------------------------ */
+static float inv_sqrt_var(int v) { return v != 0 ? 1.0f / sqrtf((float)v) : 0.0f; }
+
 void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, int D, const int* vs,
                     const int* sn, int aw, float bl, int K, int z, float* vol) {
   int r = K / 2, nk = K * K;
@@ -357,10 +360,10 @@ void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, 
       if (rin)
         for (int j = -r; j <= r; j++)
           for (int i = -r; i <= r; i++) {
-            int a = qr[(long)(y + j) * W + x + i];
+            int a = qr[(long)(y + j) * W + x + i] - 128;
             Sr += a; Srr += a * a;
           }
-      int vr = nk * Srr - Sr * Sr;
+      float sr = inv_sqrt_var(nk * Srr - Sr * Sr);
       for (int dl = 0; dl < D; dl++) {
         float d = levels[dl];
         float best = -INFINITY;
@@ -375,20 +378,16 @@ void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, 
           int Sp = 0, Spp = 0, Srp = 0;
           for (int j = -r; j <= r; j++)
             for (int i = -r; i <= r; i++) {
-              int a = qr[(long)(y + j) * W + x + i];
-              int b = qp[(long)(py + j) * W + px + i];
+              int a = qr[(long)(y + j) * W + x + i] - 128;
+              int b = qp[(long)(py + j) * W + px + i] - 128;
               Sp += b; Spp += b * b; Srp += a * b;
             }
-          int vp = nk * Spp - Sp * Sp;
-          int num = nk * Srp - Sr * Sp;
-          float ivp = vp != 0 ? 1.0f / (float)vp : 0.0f;
-          float a = (float)num;
-          float e = a * fabsf(a);
-          e = e * ivp;
+          float sp = inv_sqrt_var(nk * Spp - Sp * Sp);
+          float ap = (float)nk * sp, bp = (float)Sp * sp;
+          float e = fmaf(-(float)Sr, bp, (float)Srp * ap);
           if (e > best) best = e;
         }
-        float ivr = vr != 0 ? 1.0f / (float)vr : 0.0f;
-        float E = best * ivr;
+        float E = best * sr;
         if (!(E > -1.0f)) E = -1.0f;
         vol[((long)dl * H + y) * W + x] = 1.0f - E;
       }

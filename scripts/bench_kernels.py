@@ -57,6 +57,8 @@ def main():
     if run("ncc"):
         out["ncc_volume_1view"] = timeit(lambda: e.ncc_volume(l8, box, cam, 2, 5, out=vol))
         out["ncc_volume_view0"] = timeit(lambda: e.ncc_volume(l8, box, cam, 0, 5, out=vol))
+    if run("fill"):  # write floor: one pass of stores over a cost volume
+        out["fill_volume"] = timeit(lambda: vol.fill_(1.0))
     if run("wta"):
         out["wta_1view"] = timeit(lambda: e.wta(vol, lv))
     if run("sad"):

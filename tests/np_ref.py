@@ -227,20 +227,43 @@ def _box(a, r):
     return c[K:, K:] - c[:-K, K:] - c[K:, :-K] + c[:-K, :-K]
 
 
+def fma32(a, b, c):
+    """Correctly rounded float32 fma on arrays: a*b is exact in float64 and the
+    one double rounding that can differ (the float64 sum landing exactly on a
+    float32 midpoint) is resolved by the TwoSum error term."""
+    a, b, c = (np.asarray(t, f32) for t in (a, b, c))
+    p = a.astype(np.float64) * b.astype(np.float64)
+    cd = c.astype(np.float64)
+    s = p + cd
+    bb = s - p
+    err = (p - (s - bb)) + (cd - bb)
+    r = s.astype(f32)
+    rd = r.astype(np.float64)
+    other = np.nextafter(r, np.where(s > rd, f32(np.inf), f32(-np.inf)).astype(f32))
+    mid = (s != rd) & ((rd + other.astype(np.float64)) == 2 * s) & (err != 0)
+    pick = np.where(err > 0, np.maximum(r, other), np.minimum(r, other))
+    return np.where(mid, pick, r).astype(f32)
+
+
+def _inv_sqrt_var(v):
+    vf = np.where(v != 0, v, 1).astype(f32)
+    return np.where(v != 0, f32(1) / np.sqrt(vf), f32(0)).astype(f32)
+
+
 def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
     """Build-defined NCC K x K cost volume (csrc/ncc.hip header) -> [D][H][W]:
-    1 - max(-1, ivr * max over valid neighbour windows of (a|a|) ivp)."""
+    1 - max(-1, s_r * max over valid neighbour windows of
+    fma(-Sr', Sp' s_p, Srp' (n s_p))), centred sums, s = 1/sqrt(var)."""
     V, H, W = q.shape
     r, nk = K // 2, K * K
     bl = f32(bl)
-    qr = q[z].astype(np.int64)
+    qr = q[z].astype(np.int64) - 128
     rx, ry = z % aw, z // aw
     Sr = np.zeros((H, W), np.int64)
     Srr = np.zeros((H, W), np.int64)
     Sr[r:H - r, r:W - r] = _box(qr, r)
     Srr[r:H - r, r:W - r] = _box(qr * qr, r)
-    vr = nk * Srr - Sr * Sr
-    ivr = np.where(vr != 0, f32(1) / np.where(vr != 0, vr, 1).astype(f32), f32(0)).astype(f32)
+    sr = _inv_sqrt_var(nk * Srr - Sr * Sr)
     y, x = np.mgrid[0:H, 0:W]
     rin = (x - r >= 0) & (x + r < W) & (y - r >= 0) & (y + r < H)
     vol = np.zeros((len(levels), H, W), f32)
@@ -251,7 +274,7 @@ def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
             dx, dy = view % aw - rx, view // aw - ry
             tx = int(roundf(d * f32(dx)))
             ty = int(roundf((bl * d) * f32(dy)))
-            qp = q[view].astype(np.int64)
+            qp = q[view].astype(np.int64) - 128
             Sp = np.zeros((H, W), np.int64)
             Spp = np.zeros((H, W), np.int64)
             Srp = np.zeros((H, W), np.int64)
@@ -266,13 +289,13 @@ def ncc_volume(q, levels, vs, sn, aw, bl, K, z):
             Srp[r:H - r, r:W - r] = _box(qr * sh, r)
             px, py = x - tx, y - ty
             ok = rin & (px - r >= 0) & (px + r < W) & (py - r >= 0) & (py + r < H)
-            vp = nk * Spp - Sp * Sp
-            ivp = np.where(vp != 0, f32(1) / np.where(vp != 0, vp, 1).astype(f32), f32(0)).astype(f32)
-            a = (nk * Srp - Sr * Sp).astype(f32)
-            e = (a * np.abs(a)) * ivp
+            sp = _inv_sqrt_var(nk * Spp - Sp * Sp)
+            ap = (f32(nk) * sp).astype(f32)
+            bp = (Sp.astype(f32) * sp).astype(f32)
+            e = fma32(-Sr.astype(f32), bp, (Srp.astype(f32) * ap).astype(f32))
             best = np.where(ok & (e > best), e, best).astype(f32)
         with np.errstate(invalid="ignore"):
-            E = (best * ivr).astype(f32)  # -inf * 0 = NaN: no valid window
+            E = (best * sr).astype(f32)  # -inf * 0 = NaN: no valid window
         vol[dl] = f32(1) - np.where(E > f32(-1), E, f32(-1)).astype(f32)
     return vol
 

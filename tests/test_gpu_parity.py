@@ -125,13 +125,9 @@ def test_grid_and_pixel_sad(engine, name):
     assert_bits(sp.cpu().numpy()[..., 7], want, "grid sweep == per-pixel sweep")
 
 
-@pytest.mark.parametrize("path", ["mfma", "vector"])
 @pytest.mark.parametrize("K", [5, 7])
 @pytest.mark.parametrize("name", ["c2x1_pix", "c2x2_pix", "c3x1_pix_odd", "c5x1_ncc", "c4x1_ncc_d40", "c3x1_inc3"])
-def test_ncc_volume_and_wta(engine, name, K, path, monkeypatch):
-    # "mfma": horizontal arrays take the opt-in matrix-core sweep (k_ncc_mfma),
-    # the 2x2 array still the vector sweep; "vector": k_ncc_volume everywhere
-    monkeypatch.setenv("MVS_NCC_MFMA", "1" if path == "mfma" else "0")
+def test_ncc_volume_and_wta(engine, name, K):
     if name == "c5x1_ncc":
         c = dict(aw=5, ah=1, W=150, H=70, dmin=0, dmax=20, bl=1.0, nh=4, nv=0, seed=23)
     elif name == "c4x1_ncc_d40":  # odd width, 40 levels, |dx| up to 3 (partial residue tiles)

@@ -12,7 +12,7 @@ import pytest
 
 import oracle.oracle as orc
 from cases import CASES, PIXEL_CASES, build
-from np_ref import (assign, boundary, cvt_f64, grid_labels, l8, ncc_volume, suppress, sweep_pixel_sad, update,
+from np_ref import (fma32, assign, boundary, cvt_f64, grid_labels, l8, ncc_volume, suppress, sweep_pixel_sad, update,
                     wta)
 
 
@@ -190,6 +190,32 @@ def test_ncc_volume_bit_exact(name, K):
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), z
 
 
+def test_fma32_correctly_rounded():
+    """np_ref.fma32 (the NCC restatement's fma) equals the exactly rounded
+    a*b+c, including sums that land on a float32 rounding midpoint."""
+    from fractions import Fraction
+    rng = np.random.default_rng(3)
+    a = rng.standard_normal(4000).astype(np.float32)
+    b = rng.standard_normal(4000).astype(np.float32)
+    c = rng.standard_normal(4000).astype(np.float32)
+    # midpoint cases: c = -(a*b) rounded + a tiny remainder
+    c[:1000] = (-(a[:1000].astype(np.float64) * b[:1000])).astype(np.float32)
+    a[1000:1100] = np.float32(1 + 2 ** -12)
+    b[1000:1100] = np.float32(1 + 2 ** -12)
+    c[1000:1100] = np.float32(2 ** 20)
+    got = fma32(a, b, c)
+    for i in range(len(a)):
+        exact = Fraction(float(a[i])) * Fraction(float(b[i])) + Fraction(float(c[i]))
+        lo = np.float32(float(exact))
+        cands = [lo, np.nextafter(lo, np.float32(np.inf)), np.nextafter(lo, np.float32(-np.inf))]
+        errs = [abs(Fraction(float(t)) - exact) for t in cands]
+        m = min(errs)
+        best = [t for t, e in zip(cands, errs) if e == m]
+        if len(best) > 1:  # tie: even mantissa
+            best = [t for t in best if (t.view(np.uint32) & 1) == 0]
+        assert got[i].view(np.uint32) == best[0].view(np.uint32), (i, a[i], b[i], c[i])
+
+
 def test_ncc_cost_range_and_identity():
     """Costs lie in [0, 2]; a view matched against an identical neighbour at
     zero shift costs 1 - 1 = 0 wherever it is textured."""
@@ -199,7 +225,7 @@ def test_ncc_cost_range_and_identity():
     vs = np.array([[1, 0], [0, 0]], np.int32)
     sn = np.array([1, 1], np.int32)
     vol = orc.ncc_volume(q, np.array([0, 1, 2], np.float32), vs, sn, 2, 1.0, 5, 0)
-    assert vol.min() >= -1e-6 and vol.max() <= 2  # e = (a|a|/vr)/vp rounds to 1+ulp
+    assert vol.min() >= -1e-6 and vol.max() <= 2  # E = x s_r may round to 1+ulp
     inner = vol[0, 2:-2, 2:-2]
     assert np.allclose(inner, 0, atol=1e-6)
     assert (vol[0, :2] == 2).all() and (vol[0, :, :2] == 2).all()

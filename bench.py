@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cost", default=None, choices=["ncc", "sad"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--concurrent", action="store_true",
+                    help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py)")
     args = ap.parse_args()
 
     import torch
@@ -90,7 +92,7 @@ def main():
     rgbx = torch.from_numpy(stack).to(e.device)
     vlists = (params.nearest_neighbours(cfg["aw"], cfg["ah"], cfg["knn"]) if cfg.get("knn") else None)
     pipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=cost, refine=bool(cfg.get("refine")),
-                    filt=bool(cfg.get("filt")) and not sharded)
+                    filt=bool(cfg.get("filt")) and not sharded, concurrent=args.concurrent)
     if sharded:
         from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
         spipe = ShardedPipeline(EngineBackend(e), st, pipe.cam, ViewGather(V), pixel_cost=cost, refine=True,

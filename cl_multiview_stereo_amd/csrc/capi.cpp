@@ -226,10 +226,22 @@ int mvs_slic_d(mvs_ctx* c, const float* lab, int V, int W, int H, const mvs_slic
   if (rc) return rc;
   float* part = mvs::update_scratch_bytes(V, W, H, S) ? (float*)scr : nullptr;
   RC(mvs::launch_init_centers(s, lab, V, W, H, S, spixl));
-  RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
-  for (int i = 0; i < p->no_iter; i++) {
-    RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl, part));
+  if (part && S % 16 == 0) {
+    // assign -> (update -> assign) x no_iter with each update's tile partials
+    // produced by the assign pass before it (one Lab read per iteration)
+    RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels,
+                                p->no_iter > 0 ? part : nullptr));
+    for (int i = 0; i < p->no_iter; i++) {
+      RC(mvs::launch_update_finalize(s, part, V, W, H, S, spixl));
+      RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels,
+                                  i + 1 < p->no_iter ? part : nullptr));
+    }
+  } else {
     RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
+    for (int i = 0; i < p->no_iter; i++) {
+      RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl, part));
+      RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
+    }
   }
   if (p->enforce_connectivity) {
     uint32_t* tmp = (uint32_t*)scr;

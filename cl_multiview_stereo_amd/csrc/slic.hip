@@ -319,6 +319,120 @@ __global__ __launch_bounds__(256) void k_update_tiles(const float4* __restrict__
   }
 }
 
+// ---- assignment fused with the next update's tile partials ----------------
+// (S % 16 == 0) One wave per 16x16 image tile: the tile lies inside one
+// superpixel cell, so every candidate centre of its pixels is one of the 3x3
+// cells around it (staged in LDS per wave).  The wave assigns its 256 pixels
+// exactly as k_assign (same arithmetic, same tie rule), stores the labels
+// and, when part != nullptr, reduces the tile for each covering superpixel
+// exactly as k_update_tiles would from those labels -- one read of Lab per
+// SLIC iteration instead of two.
+__global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__ lab,
+                                                      const float* __restrict__ spixl, int W, int H, int S, int mw,
+                                                      int mh, float xy_n, float col_n, float weight, int G, int cpl,
+                                                      int ntx, int nty, uint32_t* __restrict__ labels,
+                                                      float* __restrict__ part) {
+  __shared__ float4 cxyla[4][9];  // (cx, cy, L, a) of the 3x3 cells around the tile's cell
+  __shared__ float cbb[4][9];     // b
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile = blockIdx.x * 4 + wave, z = blockIdx.y;
+  if (tile >= ntx * nty) return;  // whole wave; no workgroup barriers below
+  const int TX = tile % ntx, TY = tile / ntx, s16 = S / 16;
+  const int cxg = TX / s16, cyg = TY / s16;  // the tile's cell
+  const long P = (long)W * H;
+  const float4* L = lab + (long)z * P;
+  const float* sp = spixl + 8L * z * mw * mh;
+  if (lane < 9) {
+    const int cx = cxg - 1 + lane % 3, cy = cyg - 1 + lane / 3;
+    if (cx >= 0 && cy >= 0 && cx < mw && cy < mh) {
+      const float* c = sp + 8 * (cy * mw + cx);
+      cxyla[wave][lane] = make_float4(c[1], c[2], c[3], c[4]);
+      cbb[wave][lane] = c[5];
+    }
+  }
+  const int lx = lane & 15, ly0 = lane >> 4;  // local index k = lane + 64*m, as the reference tile
+  uint32_t lbl[4];
+  float4 c[4];
+  float fx[4], fy[4];
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int px = TX * 16 + lx, py = TY * 16 + ly0 + 4 * m;
+    const bool in = px < W && py < H;
+    c[m] = in ? L[(long)py * W + px] : make_float4(0.f, 0.f, 0.f, 0.f);
+    fx[m] = (float)px;
+    fy[m] = (float)py;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const unsigned M = 0xffffffffu / (unsigned)S + 1u;  // n / S, exact for n < 2^16, S <= 96
+  auto divS = [&](int n) { return (int)__umulhi((unsigned)n, M); };
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int col = TX * 16 + lx, row = TY * 16 + ly0 + 4 * m;
+    lbl[m] = 0xffffffffu;
+    if (col >= W || row >= H) continue;
+    const int dX = divS(col + S / 2) - cxg, dY = divS(row + S / 2) - cyg;
+    float best2 = 0.0f, min_id = -1.0f;
+    bool have = false;
+#pragma unroll
+    for (int ii = 0; ii < 2; ii++)
+#pragma unroll
+      for (int jj = 0; jj < 2; jj++) {  // i spans the x delta but offsets y (Appendix A #2), as k_assign
+        const int ox = jj - 1 + dY, oy = ii - 1 + dX;
+        const int cx = cxg + ox, cy = cyg + oy;
+        const bool ok = cx >= 0 && cy >= 0 && cx < mw && cy < mh;
+        const int e = (oy + 1) * 3 + (ox + 1);
+        const float d2 = slic_dist2(c[m], row, col, cxyla[wave][e], cbb[wave][e], weight, xy_n, col_n);
+        bool take;
+        if (!have) {
+          take = d2 < 9.0e11f || sqrtf(d2) < 999999.9999f;
+        } else if (d2 >= best2) {
+          take = false;
+        } else if (d2 < best2 * 0.99999905f) {
+          take = true;
+        } else {
+          take = sqrtf(d2) < sqrtf(best2);
+        }
+        take = take && ok;
+        best2 = take ? d2 : best2;
+        min_id = take ? (float)(cy * mw + cx) : min_id;
+        have = have || take;
+      }
+    lbl[m] = (uint32_t)min_id;
+    labels[(long)z * P + (long)row * W + col] = lbl[m];
+  }
+  if (!part) return;
+  float* out = part + (long)z * mw * mh * G * 6;
+  for (int gy = cyg - 1; gy <= cyg + 1; gy++) {
+    if (gy < 0 || gy >= mh) continue;
+    for (int gx = cxg - 1; gx <= cxg + 1; gx++) {
+      if (gx < 0 || gx >= mw) continue;
+      const uint32_t spi = (uint32_t)(gy * mw + gx);
+      const int t = (TY - (gy - 1) * s16) * cpl + (TX - (gx - 1) * s16);
+      bool mem[4], any = false;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        mem[m] = lbl[m] == spi;
+        any |= mem[m];
+      }
+      float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (__any(any)) {
+        r[0] = wave_tree(mem[0] ? fx[0] : 0.f, mem[1] ? fx[1] : 0.f, mem[2] ? fx[2] : 0.f, mem[3] ? fx[3] : 0.f);
+        r[1] = wave_tree(mem[0] ? fy[0] : 0.f, mem[1] ? fy[1] : 0.f, mem[2] ? fy[2] : 0.f, mem[3] ? fy[3] : 0.f);
+        r[2] = wave_tree(mem[0] ? c[0].x : 0.f, mem[1] ? c[1].x : 0.f, mem[2] ? c[2].x : 0.f, mem[3] ? c[3].x : 0.f);
+        r[3] = wave_tree(mem[0] ? c[0].y : 0.f, mem[1] ? c[1].y : 0.f, mem[2] ? c[2].y : 0.f, mem[3] ? c[3].y : 0.f);
+        r[4] = wave_tree(mem[0] ? c[0].z : 0.f, mem[1] ? c[1].z : 0.f, mem[2] ? c[2].z : 0.f, mem[3] ? c[3].z : 0.f);
+        r[5] = wave_tree(mem[0] ? 1.f : 0.f, mem[1] ? 1.f : 0.f, mem[2] ? 1.f : 0.f, mem[3] ? 1.f : 0.f);
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int ch = 0; ch < 6; ch++) out[((long)spi * G + t) * 6 + ch] = r[ch];
+      }
+    }
+  }
+}
+
 __global__ void k_update_finalize(const float* __restrict__ part, int mw, int mh, int S, int G, int cpl, int ntx,
                                   int nty, float* __restrict__ spixl) {
   const int sp = blockIdx.x * blockDim.x + threadIdx.x, z = blockIdx.y;
@@ -403,6 +517,28 @@ int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, in
   hipLaunchKernelGGL(k_assign, dim3((W + AS_TW - 1) / AS_TW, (H + AS_TH - 1) / AS_TH, V), dim3(256), 0, s,
                      (const float4*)lab, spixl, W, H, S, mw, mh, xy_n, col_n, weight, labels);
   MVS_LAUNCH_CHECK("k_assign");
+  return 0;
+}
+
+int launch_assign_tiles(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
+                        float col_n, float weight, uint32_t* labels, float* part) {
+  if (S % 16 != 0) return arg_fail("SLIC fused assign needs spixl_size % 16 == 0");
+  int mw = map_dim(W, S), mh = map_dim(H, S);
+  int G = (3 * S / kLocal) * (3 * S / kLocal), cpl = S * 3 / kLocal;
+  int ntx = (W + 15) / 16, nty = (H + 15) / 16;
+  hipLaunchKernelGGL(k_assign_tiles, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, spixl, W,
+                     H, S, mw, mh, xy_n, col_n, weight, G, cpl, ntx, nty, labels, part);
+  MVS_LAUNCH_CHECK("k_assign_tiles");
+  return 0;
+}
+
+int launch_update_finalize(hipStream_t s, const float* part, int V, int W, int H, int S, float* spixl) {
+  int mw = map_dim(W, S), mh = map_dim(H, S);
+  int G = (3 * S / kLocal) * (3 * S / kLocal), cpl = S * 3 / kLocal;
+  int ntx = (W + 15) / 16, nty = (H + 15) / 16;
+  hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 63) / 64, V), dim3(64), 0, s, part, mw, mh, S, G, cpl, ntx,
+                     nty, spixl);
+  MVS_LAUNCH_CHECK("k_update_finalize");
   return 0;
 }
 

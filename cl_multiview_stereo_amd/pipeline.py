@@ -32,13 +32,15 @@ class SLIC:
 
     def do_super_pixel_seg(self, rgbx: torch.Tensor):
         lab, l8 = self.e.cvt(rgbx, want_l8=True)
+        spixl, labels = self.segment(lab)
+        return lab, l8, spixl, labels
+
+    def segment(self, lab: torch.Tensor):
+        """The SLIC loop on converted views (everything after cvt)."""
         S = self.st.spixl_size
         if S == 1:
-            spixl, labels = self.e.grid(lab, 1)
-        else:
-            spixl, labels = self.e.slic(lab, S, self.st.slic_color_weight, self.st.no_iter,
-                                        self.st.enforce_connectivity)
-        return lab, l8, spixl, labels
+            return self.e.grid(lab, 1)
+        return self.e.slic(lab, S, self.st.slic_color_weight, self.st.no_iter, self.st.enforce_connectivity)
 
 
 class PhotoConsistency:
@@ -119,11 +121,20 @@ class Pipeline:
 
     The reference's exe_pipeline runs SLIC only (perform_depth_est is commented
     out, pipeline.cpp:60-64); this pipeline wires the depth stages in the order
-    of pipeline::perform_depth_est (pipeline.cpp:108-175)."""
+    of pipeline::perform_depth_est (pipeline.cpp:108-175).
+
+    concurrent=True: after the colour conversion the superpixel chain (SLIC,
+    extents, superpixel sweep: latency/L2-bound gathers) runs on a second HIP
+    stream with its own libmvs context, beside the per-pixel chain (window
+    planes, NCC volume, WTA: VALU- and HBM-bound) on the caller's stream; the
+    caller's stream joins the side stream before refinement.  Measured at C2:
+    1 % more Mpix/s, the NCC kernel 0.42 -> 0.56 ms while it shares the GPU
+    and the WTA pass 0.73 -> 0.70 of the HBM roofline, so it is off by
+    default (bench.py --concurrent)."""
 
     def __init__(self, engine: Engine, settings: params.Settings, W: int, H: int,
                  view_subset: list[list[int]] | None = None, pixel_cost: str | None = "ncc",
-                 refine: bool = False, filt: bool = False):
+                 refine: bool = False, filt: bool = False, concurrent: bool = False):
         self.e, self.st, self.W, self.H = engine, settings, W, H
         vs = view_subset if view_subset is not None else params.neighbour_lists(
             settings.array_width, settings.array_height, settings.neib_hor, settings.neib_ver)
@@ -135,6 +146,11 @@ class Pipeline:
         self.pixel = PixelSweep(engine, self.cam, W, H, pixel_cost, settings.window) if pixel_cost else None
         self.refiner = DepthRefinement(engine, self.cam, settings.spixl_size) if refine else None
         self.filter = ConsistencyFilter(engine, settings.array_width, settings.bl_ratio, settings.fuse) if filt else None
+        self.side = None
+        if concurrent and self.pixel is not None:
+            side_engine = Engine(engine.device.index)  # own context: own scratch, metadata and plans
+            self.side = (torch.cuda.Stream(engine.device), SLIC(side_engine, settings),
+                         PhotoConsistency(side_engine, self.cam, settings.spixl_size))
 
     def exe_pipeline(self, rgbx: torch.Tensor, z0: int = 0, z1: int | None = None,
                      gather=None) -> StepOutput:
@@ -142,11 +158,26 @@ class Pipeline:
         process owns; `gather` (distributed.py) all-gathers per-view maps."""
         V = rgbx.shape[0]
         z1 = V if z1 is None else z1
-        lab, l8, spixl, labels = self.slic.do_super_pixel_seg(rgbx)
-        spixl, rep = self.photo.do_initial_depth_estimation(lab, spixl, labels, z0, z1)
-        out = StepOutput(lab, spixl, labels, rep)
-        if self.pixel is not None:
-            out.disp, out.conf = self.pixel.run(lab, l8, z0, z1)
+        if self.side is None:
+            lab, l8, spixl, labels = self.slic.do_super_pixel_seg(rgbx)
+            spixl, rep = self.photo.do_initial_depth_estimation(lab, spixl, labels, z0, z1)
+            out = StepOutput(lab, spixl, labels, rep)
+            if self.pixel is not None:
+                out.disp, out.conf = self.pixel.run(lab, l8, z0, z1)
+        else:
+            lab, l8 = self.e.cvt(rgbx, want_l8=True)
+            main = torch.cuda.current_stream(self.e.device)
+            stream, slic, photo = self.side
+            stream.wait_stream(main)
+            with torch.cuda.stream(stream):
+                spixl, labels = slic.segment(lab)
+                spixl, rep = photo.do_initial_depth_estimation(lab, spixl, labels, z0, z1)
+            lab.record_stream(stream)  # allocated on main, read on the side stream
+            disp, conf = self.pixel.run(lab, l8, z0, z1)
+            main.wait_stream(stream)
+            for t in (spixl, labels, rep):  # allocated on the side stream, used on main from here
+                t.record_stream(main)
+            out = StepOutput(lab, spixl, labels, rep, disp, conf)
         if self.refiner is not None:
             r = self.refiner.do_refinement(spixl, labels, rep, self.st)
             out.disp_refined = r["disp"]

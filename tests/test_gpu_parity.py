@@ -291,3 +291,25 @@ def test_slic_ties(engine, kind):
         _, osp, olb = orc.slic(rgbx[0], S_)
         assert_bits(as_u32(lb)[0], olb, f"{kind} labels S={S_}")
         assert_bits(sp.cpu().numpy()[0][..., :7], osp[..., :7], f"{kind} spixl S={S_}")
+
+
+@pytest.mark.parametrize("name", ["c3x1_s16", "c3x3_s8"])
+def test_concurrent_pipeline_matches_serial(engine, name):
+    """Pipeline(concurrent=True) runs the superpixel chain on a second stream
+    and context: every output equals the one-stream pipeline's bit for bit."""
+    from cl_multiview_stereo_amd.pipeline import Pipeline
+    c = CASES[name]
+    b = build(c)
+    st = params.Settings(spixl_size=c["S"], array_width=c["aw"], array_height=c["ah"], min_disp=c["dmin"],
+                         max_disp=c["dmax"], inc=1, neib_hor=c["nh"], neib_ver=c["nv"], bl_ratio=c["bl"], window=5,
+                         cost="ncc")
+    rgbx = dev(b["stack"])
+    outs = []
+    for conc in (False, True):
+        p = Pipeline(engine, st, c["W"], c["H"], concurrent=conc)
+        o = p.exe_pipeline(rgbx)
+        o = p.exe_pipeline(rgbx)  # twice: the second run reuses cached allocator blocks across streams
+        torch.cuda.synchronize()
+        outs.append(o)
+    for f in ("spixl", "labels", "rep", "disp", "conf"):
+        assert_bits(getattr(outs[1], f).cpu().numpy(), getattr(outs[0], f).cpu().numpy(), f)

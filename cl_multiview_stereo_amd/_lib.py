@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmvs.so")
+# MVS_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("MVS_LIB") or os.path.join(_HERE, "libmvs.so")
 
 # every symbol include/mvs.h declares (checked by tests/test_boundary.py)
 EXPORTS = [

@@ -306,7 +306,7 @@ __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
-__global__ __launch_bounds__(256) void k_propagate(RArgs c, const float* __restrict__ spixl,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_propagate(RArgs c, const float* __restrict__ spixl,
                                                    const uint32_t* __restrict__ labels,
                                                    const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
                                                    const int* __restrict__ vs, const int* __restrict__ sn, int iter,

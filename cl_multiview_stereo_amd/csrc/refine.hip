@@ -760,8 +760,10 @@ int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fu
   if (z1 > z0) {
     const dim3 g((W + 255) / 256, H, z1 - z0);
     const dim3 gp((W + 255) / 256, H);
+    // few views: one thread per (reference, pixel) keeps more threads in flight
+    // (measured at V = 5: 350 vs 395 us); many views: one thread per pixel
     if (V <= 8)
-      hipLaunchKernelGGL(k_remove_incons_px<8>, gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1, out);
+      hipLaunchKernelGGL(k_remove_incons_sel<8>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
     else if (V <= 16)
       hipLaunchKernelGGL(k_remove_incons_px<16>, gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1, out);
     else if (V <= 32)

@@ -294,6 +294,58 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
   return finish_consistency(cons, vc);
 }
 
+// compute_consistency's sums for ONE neighbour view k (samples in order,
+// each view's sums start at 0 as in the reference): {num, vis_w, occ_w,
+// visibility, visible}.  Same arithmetic as comp_consistency.
+__device__ void view_sums(const PCtx& p, float d, float nx, float ny, float nz, int k, float* o) {
+  const RArgs& c = p.c;
+  const long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
+  const int camx = p.z % c.aw, camy = p.z / c.aw;
+  const int cxi = (int)p.cx, cyi = (int)p.cy;
+  const int view = p.vs[c.V * p.z + k];
+  const float fdx = (float)(view % c.aw - camx), fdy = (float)(view / c.aw - camy);
+  const uint32_t* lv = p.labels + P * view;
+  int xp[9], yp[9];
+  bool ok[9];
+  uint32_t ip[9];
+  float di[9];
+#pragma unroll
+  for (int s = 0; s < 9; s++) {
+    const float sxf = (float)(cxi + p.smp[s] * (s / 3 - 1));
+    const float syf = (float)(cyi + p.smp[s] * (s % 3 - 1));
+    di[s] = plane_at(nx, ny, nz, p.cx, p.cy, d, sxf, syf);
+    xp[s] = (int)(sxf - roundf(di[s] * fdx));
+    yp[s] = (int)(syf - roundf((c.bl * di[s]) * fdy));
+    ok[s] = xp[s] >= 0 && yp[s] >= 0 && xp[s] < c.W && yp[s] < c.H;
+    ip[s] = lv[ok[s] ? (long)c.W * yp[s] + xp[s] : 0];
+  }
+  float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 9; s++) {
+    const long q = M * view + ip[s];
+    const float4 sa = *(const float4*)(p.spixl + 8 * q);
+    const float2 sb = *(const float2*)(p.spixl + 8 * q + 4);
+    const float* sq = p.st + 6 * q;
+    const float2 t0 = *(const float2*)(sq);
+    const float2 t1 = *(const float2*)(sq + 2);
+    const float2 t2 = *(const float2*)(sq + 4);
+    float dip = plane_at(t1.y, t2.x, t2.y, sa.y, sa.z, t0.x, (float)xp[s], (float)yp[s]);
+    float diff = dip - di[s];
+    const float wv = fabsf(diff) < c.fuse ? 1.0f : 0.0f;
+    const float t_vis = wv * expf_neg_sq(diff, c.alpha);
+    diff = mvs_distance3(sa.w, sb.x, sb.y, p.col[0], p.col[1], p.col[2]);
+    const float t_col = expf_neg_sq(diff, c.gamma);
+    if (ok[s]) {
+      visible = visible + t_vis;
+      vis_w = vis_w + wv;
+      occ_w = occ_w + (1.0f - wv);
+      visibility = visibility + t_col;
+      num = num + 1.0f;
+    }
+  }
+  o[0] = num; o[1] = vis_w; o[2] = occ_w; o[3] = visibility; o[4] = visible;
+}
+
 // One WAVE per superpixel.  The reference evaluates its candidate planes one
 // after another, but a candidate's (sm, cs) never depends on the running
 // state -- only the accept test does -- so lanes evaluate the candidates in
@@ -302,6 +354,7 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
 // in the reference's order over the broadcast results: bit-identical, with
 // the superpixel count of waves in flight instead of that many threads.
 // k is wave-uniform at every call: a v_readlane into an SGPR, not an LDS permute
+constexpr int kTriViews = 8;  // views the lane-parallel triangle phase keeps in LDS
 __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
@@ -424,8 +477,87 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
   }
 
-  // spatialRefinement over the 8 neighbour triangles (clcode.cl:1676-1723, 1808-1820)
-  {
+  // spatialRefinement over the 8 neighbour triangles (clcode.cl:1676-1723, 1808-1820).
+  // Lane-parallel form (fast smoothness terms, <= kTriViews views): lane 8t+r
+  // works for triangle t.  The smoothness products simi_l * exp(...) are
+  // computed by lanes r = l mod 8 into LDS and summed in term order by lane 8t;
+  // each view's consistency sums (9 samples in order) by lane r = view mod 8,
+  // combined in view order by lane 8t -- every float sum in the reference's
+  // order, so bit-identical to the one-lane-per-triangle form kept below.
+  const int nv = sn[z];
+  if (fast_sm && nv <= kTriViews) {
+    __shared__ float s_prod[4][8][64];
+    __shared__ float s_view[4][8][kTriViews][5];
+    const int w = threadIdx.x >> 6;
+    const int t = lane >> 3, r = lane & 7;
+    const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
+    const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
+    const int u = (t + 1) % 8;
+    const bool ok = nbx[t] > -1 && nby[t] > -1 && nbx[t] < c.mw && nby[t] < c.mh && nbx[u] > -1 && nby[u] > -1 &&
+                    nbx[u] < c.mw && nby[u] < c.mh;
+    float n0 = 0.f, n1 = 0.f, n2 = 0.f;
+    if (ok) {
+      const long q1 = M * z + (long)c.mw * nby[t] + nbx[t], q2 = M * z + (long)c.mw * nby[u] + nbx[u];
+      const float* a1 = spixl + 8 * q1;
+      const float* a2 = spixl + 8 * q2;
+      const float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = st_in[6 * q1] - cur.d;
+      const float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = st_in[6 * q2] - cur.d;
+      n0 = v1y * v2z - v1z * v2y;
+      n1 = v2x * v1z - v1x * v2z;
+      n2 = v1x * v2y - v1y * v2x;
+      float ss = n0 * n0;
+      ss = ss + n1 * n1;
+      ss = ss + n2 * n2;
+      ss = ss + 0.0f * 0.0f;
+      if (ss != 0.0f) {
+        const float rr = sqrtf(ss);
+        n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
+      }
+    }
+    // smoothness products; uniform trip count so every lane takes part in the shuffles
+    for (int i = 0; i < (nterm + 7) / 8; i++) {
+      const int l = r + 8 * i;
+      const int ls = l < 64 ? l : 0;
+      const float simi = __shfl(t_simi, ls), sx = __shfl(t_sx, ls), sy = __shfl(t_sy, ls), sd = __shfl(t_sd, ls);
+      if (ok && l < nterm && ((t_valid >> l) & 1ull)) {
+        const float di = plane_at(n0, n1, n2, p.cx, p.cy, cur.d, sx, sy);
+        const float diff = di - sd;
+        s_prod[w][t][l] = simi * expf_neg_sq(diff, c.alpha);
+      }
+    }
+    for (int k = r; k < nv; k += 8)
+      if (ok) view_sums(p, cur.d, n0, n1, n2, k, s_view[w][t][k]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float sm1 = 0.f, cs1 = 0.f;
+    if (ok && r == 0) {
+      float sm = 0.0f;
+      for (int l = 0; l < nterm; l++)
+        if ((t_valid >> l) & 1ull) sm = sm + s_prod[w][t][l];
+      sm1 = wn > 0 ? sm / wn : 0.000001f;
+      float cons = 0.0f;
+      int vc = 0;
+      for (int k = 0; k < nv; k++) {
+        const float* o = s_view[w][t][k];
+        const float num = o[0], vis_w = o[1], occ_w = o[2], visibility = o[3], visible = o[4];
+        if (num > 0) {
+          vc++;
+          if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+          if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)p.fl.y);
+        }
+      }
+      cs1 = finish_consistency(cons, vc);
+    }
+    const unsigned long long valid = __ballot(ok && r == 0);
+    for (int l = 0; l < 8; l++) {
+      if (!((valid >> (8 * l)) & 1ull)) continue;
+      const float ksm = bcast(sm1, 8 * l), kcs = bcast(cs1, 8 * l);
+      if ((iter < 4 && ksm > cur.sm) || ksm * kcs > cur.sm * cur.cs) {
+        cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, 8 * l); cur.ny = bcast(n1, 8 * l); cur.nz = bcast(n2, 8 * l);
+      }
+    }
+  } else {
     const int t = lane & 7;
     const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
     const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
@@ -447,8 +579,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       ss = ss + n2 * n2;
       ss = ss + 0.0f * 0.0f;
       if (ss != 0.0f) {
-        const float r = sqrtf(ss);
-        n0 = n0 / r; n1 = n1 / r; n2 = n2 / r;
+        const float rr = sqrtf(ss);
+        n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
       }
       sm1 = smooth(cur.d, n0, n1, n2);
       cs1 = comp_consistency(p, cur.d, n0, n1, n2);

@@ -13,6 +13,8 @@ CASES = {
     "c2x2_s12": dict(aw=2, ah=2, W=90, H=61, S=12, dmin=0, dmax=9, bl=1.0359, nh=1, nv=1, seed=19),
     "c5x1_s32": dict(aw=5, ah=1, W=200, H=150, S=32, dmin=0, dmax=31, bl=1.0, nh=4, nv=0, seed=17),
     "c2x1_s40": dict(aw=2, ah=1, W=250, H=170, S=40, dmin=0, dmax=7, bl=1.0, nh=1, nv=0, seed=18),
+    # up to 14 neighbours per view: the refinement's > 8-view (one lane per triangle) path
+    "c5x3_s16": dict(aw=5, ah=3, W=96, H=64, S=16, dmin=0, dmax=11, bl=1.0359, nh=2, nv=1, seed=20),
 }
 
 PIXEL_CASES = {

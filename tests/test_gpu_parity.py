@@ -153,21 +153,23 @@ def test_ncc_volume_and_wta(engine, name, K):
         assert_bits(conf.cpu().numpy(), oc, "wta conf")
 
 
-@pytest.mark.parametrize("name,ks", [("c3x3_s8", 26), ("c3x1_s16", 52), ("c5x1_s32", 1080), ("c3x1_s8", 1080)])
-def test_refinement(engine, name, ks):
+@pytest.mark.parametrize("name,ks,kst", [("c3x3_s8", 26, 13), ("c3x1_s16", 52, 13), ("c5x1_s32", 1080, 13),
+                                         ("c3x1_s8", 1080, 13), ("c5x3_s16", 1080, 13),
+                                         ("c3x1_s8", 1080, 16)])  # kernel_step 16: > 64 smoothness terms
+def test_refinement(engine, name, ks, kst):
     c = CASES[name]
     b = build(c)
     lab, sp, lb, rep = _chain(engine, c, b)
     cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
     engine.sweep_spixl(lab, sp, rep, cam, c["S"])
     sp_h, lb_h, rep_h = sp.cpu().numpy(), as_u32(lb), rep.cpu().numpy()
-    want = orc.refine(sp_h, lb_h, rep_h, b["vs"], b["sn"], c["aw"], c["bl"], c["S"], 2.0, 6.0, 1.0, 13, ks, 5, True)
-    got = engine.refine(sp, lb, rep, cam, c["S"], 2.0, 6.0, 1.0, 13, ks, 5, True)
+    want = orc.refine(sp_h, lb_h, rep_h, b["vs"], b["sn"], c["aw"], c["bl"], c["S"], 2.0, 6.0, 1.0, kst, ks, 5, True)
+    got = engine.refine(sp, lb, rep, cam, c["S"], 2.0, 6.0, 1.0, kst, ks, 5, True)
     assert_bits(got["flat"].cpu().numpy(), want["flat"], "flatness")
     assert_bits(got["state_compat"].cpu().numpy(), want["states"][3], "state after iteration 3 (fusion input)")
     assert_bits(got["disp"].cpu().numpy(), want["disp"], "fused disparity")
     # per-stage: init state and each propagate iteration
-    rp = params.refine_params(params.Settings(spixl_size=c["S"], kernel_size=ks))
+    rp = params.refine_params(params.Settings(spixl_size=c["S"], kernel_size=ks, kernel_step=kst))
     flat = engine.flatness(sp, rp["flat_gamma"])
     st = engine.init_state(sp, lb, rep, flat, cam, c["S"], rp["init_gamma"], rp["init_alpha"], rp["kernel_steps"],
                            rp["kss"], rp["fuse"])

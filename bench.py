@@ -194,6 +194,20 @@ def main():
                                  "unit_view_cells": "G view-cells/s",
                                  "hbm_write_GBps": round(vol_bytes / t_ncc / 1e9, 1),
                                  "hbm_write_frac": round(vol_bytes / t_ncc / 1e9 / HBM_PEAK_GBS, 4)}
+        # VALU issue bound of the producer (its binding resource): wave-instructions per
+        # launch from the SQ_INSTS_VALU pass (profiles/pmc_ncc.json, C2) at one
+        # instruction per 4 cycles per SIMD, 1024 SIMDs, 2.4 GHz
+        pmc_ncc = os.path.join(ROOT, "profiles", "pmc_ncc.json")
+        if args.config == "c2" and cost == "ncc" and os.path.exists(pmc_ncc):
+            try:
+                ent = [v for k, v in json.load(open(pmc_ncc)).items() if k.startswith("k_ncc_volume")]
+                insts = sum(e["valu_wave_insts_per_launch"] for e in ent) / len(ent)
+                peak = 1024 * 2.4e9 / 4.0
+                res["roofline_sweep"].update({"bound": "valu", "valu_wave_insts_per_launch": round(insts),
+                                              "valu_issue_frac": round(insts / t_ncc / peak, 4),
+                                              "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op"})
+            except Exception:
+                pass
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg.get("refine"):
         try:

@@ -43,18 +43,22 @@ def main():
         for r in rows:
             w.writerow([short(r[0]), r[1], round(r[2], 1), round(r[3], 1), round(r[4], 3)])
     pmc = defaultdict(dict)
-    for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+    for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write"), ("SQ_INSTS_VALU", "pmc_valu"),
+                         ("SQ_INSTS_LDS", "pmc_valu")):
         d = db(os.path.join(src, sub))
         if d is None:
             continue
         acc = defaultdict(list)
+        scale, unit = (1024.0, "_bytes_per_launch") if counter.endswith("SIZE") else (1.0, "_per_launch")
         for name, val in d.execute("select kernel_name, value from counters_collection where counter_name=?",
                                    (counter,)):
-            acc[short(name)].append(val * 1024.0)  # counters are KB
+            acc[short(name)].append(val * scale)  # FETCH/WRITE_SIZE are KB; SQ_INSTS_* wave-instructions
         for k, v in acc.items():
-            pmc[k][counter + "_bytes_per_launch"] = sum(v) / len(v)
+            pmc[k][counter + unit] = sum(v) / len(v)
             pmc[k]["launches"] = len(v)
     for k, v in pmc.items():
+        if "WRITE_SIZE_bytes_per_launch" not in v and "FETCH_SIZE_bytes_per_launch" not in v:
+            continue
         if "FETCH_SIZE_bytes_per_launch" in v:
             v["hbm_read_bytes_corrected"] = 2.0 * v["FETCH_SIZE_bytes_per_launch"]
         v["hbm_bytes_per_launch"] = v.get("hbm_read_bytes_corrected", 0.0) + v.get("WRITE_SIZE_bytes_per_launch", 0.0)
@@ -65,6 +69,12 @@ def main():
                    "hbm_bytes_per_launch": pmc[wta]["hbm_bytes_per_launch"],
                    "note": "2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes"},
                   open(os.path.join(out, "pmc_wta.json"), "w"), indent=1)
+    ncc = [k for k in sorted(pmc) if k.startswith("k_ncc_volume") and "SQ_INSTS_VALU_per_launch" in pmc[k]]
+    if ncc:
+        json.dump({k: {"valu_wave_insts_per_launch": pmc[k]["SQ_INSTS_VALU_per_launch"],
+                       "lds_wave_insts_per_launch": pmc[k].get("SQ_INSTS_LDS_per_launch")} for k in ncc} |
+                  {"source": f"profiles/{tag}_pmc.json", "note": "SQ_INSTS_VALU / SQ_INSTS_LDS, own --pmc pass"},
+                  open(os.path.join(out, "pmc_ncc.json"), "w"), indent=1)
     for r in rows[:8]:
         print(f"{short(r[0]):40s} calls={r[1]:5d} avg={r[3]:9.3f} us  {r[4]:6.2f}%")
     for k in sorted(pmc):

@@ -108,6 +108,7 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
 }
 
 constexpr int kMaxNbr = 16;
+constexpr int kCPolNT = 2;  // buffer cache policy: non-temporal (CPol::NT on gfx940+)
 struct NccArgs {
   int W, H, D, nn, z;
   int tiles_x, ntiles, tiles_per_xcd, nch;  // XCD-aware work map (see k_ncc_volume)
@@ -277,15 +278,27 @@ __global__ __launch_bounds__(NW * 64) void k_ncc_volume(const uint2* __restrict_
     for (int j = 0; j < DPW; j++) {
       const int dl = c * DC + wave + NW * j;
       if (dl >= a.D) break;
-      float* vd = vol + (long)dl * P;  // scalar base; 32-bit per-lane offsets (saddr stores)
-      const int off0 = y0 * W + x;
+      // buffer stores: the level plane as a buffer resource (scalar), the lane's
+      // byte offset fixed for the tile, the row offset scalar -- no address VALU
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(vol + (long)dl * P, 0, (int)(P * 4), 0x00020000);
+      const int off0 = (y0 * W + x) * 4;
+      // cost pairs: m*s_r as one v_pk_mul_f32, 1 - c as one v_pk_add_f32
+      float cst[TH];
+#pragma unroll
+      for (int o = 0; o < TH; o += 2) {
+        const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{sr[o], sr[o + 1]};
+        const f32x2 m = f32x2{vmax(e.x, -1.0f), vmax(e.y, -1.0f)};
+        const f32x2 r = f32x2{1.0f, 1.0f} - m;
+        cst[o] = r.x;
+        cst[o + 1] = r.y;
+      }
+      // streaming (nt) stores: the volume must not evict the neighbour bands
+      // from L2 / MALL (measured: the WTA pass after it also runs faster)
 #pragma unroll
       for (int o = 0; o < TH; o++)
-        if (y0 + o < H) {
-          // streaming store: the volume must not evict the neighbour bands
-          // from L2 / MALL (measured: the WTA pass after it also runs faster)
-          __builtin_nontemporal_store(1.0f - vmax(E[j][o] * sr[o], -1.0f), vd + off0 + o * W);
-        }
+        if (y0 + TH <= H || y0 + o < H)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(cst[o]), rs, off0, o * W * 4, kCPolNT);
     }
   };
 

@@ -40,6 +40,11 @@ CONFIGS = {
                refine=True, filt=True, sharded=True,
                workload="32 reference views x 5 nearest neighbours, 1080p, one array sharded by reference view over "
                         "the GPUs (RCCL all-gathers of labels/spixl, refinement state, disparity)"),
+    # the reference's own defaults (clMVDE.cpp main): its algorithm exactly, no per-pixel sweep
+    "ref": dict(aw=3, ah=3, W=1920, H=1080, S=8, dmin=30, dmax=60, K=5, nh=1, nv=1, bl=1.0359, cost="none",
+                refine=True,
+                workload="clMVDE main() defaults: 3x3 array 1080p, S=8 (32,400 superpixels/view), levels 30..60, "
+                         "superpixel SAD sweep + refinement (5 propagations) + fusion, all 9 views"),
     "c5": dict(aw=5, ah=1, W=4096, H=3072, S=40, dmin=0, dmax=255, K=7, nh=4, nv=0, bl=1.0, cost="ncc",
                workload="5-view 4096x3072, 256 hypotheses, NCC 7x7, SLIC K=7931 (S=40)"),
 }
@@ -56,7 +61,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cost", default=None, choices=["ncc", "sad"])
+    ap.add_argument("--cost", default=None, choices=["ncc", "sad", "none"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--concurrent", action="store_true",
                     help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py)")
@@ -91,7 +96,8 @@ def main():
                                 0x5EED + 2 + (0 if sharded else rank))
     rgbx = torch.from_numpy(stack).to(e.device)
     vlists = (params.nearest_neighbours(cfg["aw"], cfg["ah"], cfg["knn"]) if cfg.get("knn") else None)
-    pipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=cost, refine=bool(cfg.get("refine")),
+    pipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,
+                    refine=bool(cfg.get("refine")),
                     filt=bool(cfg.get("filt")) and not sharded, concurrent=args.concurrent)
     if sharded:
         from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
@@ -209,7 +215,7 @@ def main():
             except Exception:
                 pass
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg.get("refine"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and (not cfg.get("refine") or cost == "none"):
         try:
             res["cpu_baseline"], res["depth_l1_vs_oracle"] = cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out)
         except Exception as ex:  # report, never hide
@@ -241,9 +247,11 @@ def cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out):
     sp = np.stack([o[1] for o in outs])
     lb = np.stack([o[2] for o in outs])
     rep = orc.boundary(sp, lb, S)
-    orc.sweep(lab_all, sp, rep, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"], S)
+    sp = orc.sweep(lab_all, sp, rep, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"], S)
     t_seg = time.perf_counter() - t0
-    if cost == "ncc":
+    if cost == "none":  # the reference pipeline: refinement + fusion of every view
+        od = orc.refine(sp, lb, rep, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"], S)["disp"]
+    elif cost == "ncc":
         q = orc.l8(lab_all)
         od = np.stack([orc.wta(orc.ncc_volume(q, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"],
                                               cfg["K"], z), cam.levels)[0] for z in range(V)])
@@ -255,7 +263,7 @@ def cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out):
                      f"oracle/mvs_oracle.c, OpenMP x{threads}: {t_all:.1f}s (segmentation+superpixel sweep "
                      f"{t_seg:.1f}s)"}
     torch.cuda.synchronize()
-    gd = out.disp.cpu().numpy()
+    gd = (out.disp_refined if cost == "none" else out.disp).cpu().numpy()
     l1 = float(np.abs(gd - od).mean())
     return cpu, {"value": l1, "unit": "px (mean |d_gpu - d_oracle|)", "bit_exact": bool(np.array_equal(gd, od)),
                  "sample": f"the last timed step's disparity maps, all {V} reference views, {W}x{H}"}

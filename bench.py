@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--concurrent", action="store_true",
                     help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py)")
+    ap.add_argument("--fused", action="store_true",
+                    help="NCC sweep with the winner-take-all folded in (mvs_ncc_wta_d: no cost volume in HBM)")
     args = ap.parse_args()
 
     import torch
@@ -98,14 +100,14 @@ def main():
     vlists = (params.nearest_neighbours(cfg["aw"], cfg["ah"], cfg["knn"]) if cfg.get("knn") else None)
     pipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,
                     refine=bool(cfg.get("refine")),
-                    filt=bool(cfg.get("filt")) and not sharded, concurrent=args.concurrent)
+                    filt=bool(cfg.get("filt")) and not sharded, concurrent=args.concurrent, fused=args.fused)
     if sharded:
         from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
         spipe = ShardedPipeline(EngineBackend(e), st, pipe.cam, ViewGather(V), pixel_cost=cost, refine=True,
                                 filt=bool(cfg.get("filt")))
 
     # HIP events around the cost-volume kernels, on the stream they run on
-    timers = {"wta": [], "ncc": []}
+    timers = {"wta": [], "ncc": [], "fused": []}
     if pipe.pixel is not None and cost == "ncc":
         orig_wta, orig_vol = e.wta, e.ncc_volume
 
@@ -123,6 +125,7 @@ def main():
         timing = [False]
         e.wta = timed("wta", orig_wta)
         e.ncc_volume = timed("ncc", orig_vol)
+        e.ncc_wta = timed("fused", e.ncc_wta)
     else:
         timing = [False]
 
@@ -174,9 +177,33 @@ def main():
                    "refinement": bool(cfg.get("refine")), "consistency_filter": bool(cfg.get("filt"))},
     }
 
+    def avg(lst):
+        return sum(s.elapsed_time(t) for s, t in lst) / len(lst) * 1e-3
+
+    def valu_insts(fused):
+        # SQ_INSTS_VALU per launch (profiles/pmc_ncc.json, C2), launch-weighted over
+        # the band-width variants of the plain (FUSE=false) or fused kernel
+        pmc_ncc = os.path.join(ROOT, "profiles", "pmc_ncc.json")
+        if args.config != "c2" or cost != "ncc" or not os.path.exists(pmc_ncc):
+            return None
+        tag = "true>" if fused else "false>"
+        ent = [v for k, v in json.load(open(pmc_ncc)).items() if k.startswith("k_ncc_volume") and k.endswith(tag)]
+        if not ent:
+            return None
+        wts = [e.get("launches", 1) for e in ent]
+        return sum(e["valu_wave_insts_per_launch"] * w for e, w in zip(ent, wts)) / sum(wts)
+
+    VALU_PEAK = 1024 * 2.4e9 / 4.0  # wave64 VALU ops/s: 1024 SIMDs x 2.4 GHz / 4 cycles
+    if args.fused and timers["fused"]:
+        # no volume: the fused sweep is VALU-issue-bound
+        t_ncc = avg(timers["fused"])
+        insts = valu_insts(True)
+        res["roofline"] = {"bound": "valu", "kernel": "k_ncc_volume<..., FUSE=true> (sweep + WTA, no volume)",
+                           "achieved": None if insts is None else round(insts / t_ncc / 1e9, 1),
+                           "peak": VALU_PEAK / 1e9, "unit": "G wave-instructions/s",
+                           "frac": None if insts is None else round(insts / t_ncc / VALU_PEAK, 4),
+                           "traffic": None, "avg_launch_ms": round(t_ncc * 1e3, 4)}
     if timers["wta"]:
-        def avg(lst):
-            return sum(s.elapsed_time(t) for s, t in lst) / len(lst) * 1e-3
         t_wta = avg(timers["wta"])
         t_ncc = avg(timers["ncc"])
         wta_bytes = 4.0 * D * W * H + 8.0 * W * H  # volume read + disparity/confidence write
@@ -203,17 +230,45 @@ def main():
         # VALU issue bound of the producer (its binding resource): wave-instructions per
         # launch from the SQ_INSTS_VALU pass (profiles/pmc_ncc.json, C2) at one
         # instruction per 4 cycles per SIMD, 1024 SIMDs, 2.4 GHz
-        pmc_ncc = os.path.join(ROOT, "profiles", "pmc_ncc.json")
-        if args.config == "c2" and cost == "ncc" and os.path.exists(pmc_ncc):
-            try:
-                ent = [v for k, v in json.load(open(pmc_ncc)).items() if k.startswith("k_ncc_volume")]
-                insts = sum(e["valu_wave_insts_per_launch"] for e in ent) / len(ent)
-                peak = 1024 * 2.4e9 / 4.0
-                res["roofline_sweep"].update({"bound": "valu", "valu_wave_insts_per_launch": round(insts),
-                                              "valu_issue_frac": round(insts / t_ncc / peak, 4),
-                                              "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op"})
-            except Exception:
-                pass
+        insts = valu_insts(False)
+        if insts is not None:
+            res["roofline_sweep"].update({"bound": "valu", "valu_wave_insts_per_launch": round(insts),
+                                          "valu_issue_frac": round(insts / t_ncc / VALU_PEAK, 4),
+                                          "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op"})
+
+    # the same step with the WTA folded into the sweep kernel (no cost volume in
+    # HBM): timed with the same protocol after the headline run, outputs
+    # compared bit-for-bit with the headline step's
+    if cost == "ncc" and not args.fused and not sharded and not cfg.get("refine"):
+        fpipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=cost, fused=True)
+        for _ in range(max(1, args.warmup)):
+            fout = fpipe.exe_pipeline(rgbx)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        timing[0] = True
+        f0 = time.perf_counter()
+        for _ in range(args.steps):
+            fout = fpipe.exe_pipeline(rgbx)
+        torch.cuda.synchronize()
+        fel = time.perf_counter() - f0
+        timing[0] = False
+        if world > 1:
+            dist.barrier()
+            tt = torch.tensor([fel], device=e.device, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            fel = float(tt.item())
+        same = bool(torch.equal(fout.disp.view(torch.int32), out.disp.view(torch.int32)) and
+                    torch.equal(fout.conf.view(torch.int32), out.conf.view(torch.int32)))
+        res["fused_variant"] = {"what": "bench.py --fused: k_ncc_volume with the WTA folded in, no cost volume in HBM",
+                                "value": round(units * W * H * args.steps / fel / 1e6, 3), "unit": "Mpix/s",
+                                "ms_per_step": round(fel * 1e3 / max(args.steps, 1), 4),
+                                "bit_identical_to_headline": same,
+                                "sweep_avg_launch_ms": round(avg(timers["fused"]) * 1e3, 4) if timers["fused"] else None}
+        fi = valu_insts(True)
+        if fi is not None and timers["fused"]:
+            res["fused_variant"]["valu_issue_frac"] = round(fi / avg(timers["fused"]) / VALU_PEAK, 4)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline and (not cfg.get("refine") or cost == "none"):
         try:

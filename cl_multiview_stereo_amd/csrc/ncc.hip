@@ -140,6 +140,26 @@ __device__ __forceinline__ float vmax(float acc, float e) {
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(e));
   return r;
 }
+__device__ __forceinline__ float vmin(float acc, float e) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(e));
+  return r;
+}
+// median of three: with lo <= hi, med3(lo, hi, c) = min(hi, max(lo, c))
+__device__ __forceinline__ float vmed3(float lo, float hi, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(lo), "v"(hi), "v"(c));
+  return r;
+}
+
+// Fused winner-take-all outputs (k_ncc_volume<..., FUSE = true>): the volume
+// is never written.  Same results as k_wta over the materialised volume.
+struct WtaOut {
+  const float* levels;  // device [D]
+  float* disp;          // [H][W]
+  float* conf;          // [H][W] or null
+};
+constexpr float kWtaInit = 1000000.0f;  // k_wta's Top4 initial cost (sweep.hip)
 
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -202,10 +222,18 @@ __device__ __forceinline__ int dot4(unsigned a, unsigned b, int c) {
 
 // EVEN: every level's band rows start on a pair boundary (all horizontal
 // neighbours with even R + tymax): branch-free pair reads.
-template <int K, int TH, int DPW, int NW, int BW, bool EVEN>
-__global__ __launch_bounds__(NW * 64) void k_ncc_volume(const uint2* __restrict__ stats, const uint2* __restrict__ pk,
+// FUSE: instead of writing the volume, every wave folds its levels' costs into
+// a per-pixel (smallest cost, its level, second smallest cost) in level order;
+// the workgroup then merges its waves through LDS into disp/conf.  A wave's
+// levels are NW >= 4 apart, so at most one of them lies in best+-1: the
+// smallest cost outside best+-1 is, per wave, its second smallest if its best
+// level is in that window, else its smallest -- exactly what k_wta's top-4
+// yields (ties resolved to the lower level by the strict < in level order).
+template <int K, int TH, int DPW, int NW, int BW, bool EVEN, bool FUSE>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_volume(const uint2* __restrict__ stats, const uint2* __restrict__ pk,
                                                     const NccRec* __restrict__ plan, NccArgs a,
-                                                    float* __restrict__ vol) {
+                                                    float* __restrict__ vol, WtaOut wo) {
+  static_assert(!FUSE || NW >= 3, "fused WTA needs a wave's levels >= 3 apart");
   constexpr int R = K / 2;
   constexpr int NR = TH + 2 * R;
   constexpr int NK = K * K;
@@ -264,6 +292,16 @@ __global__ __launch_bounds__(NW * 64) void k_ncc_volume(const uint2* __restrict_
   };
   float E[DPW][TH];
   float sr[TH];  // reference 1/sqrt(var) per output row (NaN: invalid window)
+  float wv0[TH], wv1[TH];  // FUSE: this wave's smallest and second smallest cost per row
+  int wi0[TH];             //       level of the smallest
+  if (FUSE) {
+#pragma unroll
+    for (int o = 0; o < TH; o++) {
+      wv0[o] = kWtaInit;
+      wv1[o] = kWtaInit;
+      wi0[o] = -1;
+    }
+  }
   auto reset = [&]() {
 #pragma unroll
     for (int j = 0; j < DPW; j++)
@@ -278,6 +316,21 @@ __global__ __launch_bounds__(NW * 64) void k_ncc_volume(const uint2* __restrict_
     for (int j = 0; j < DPW; j++) {
       const int dl = c * DC + wave + NW * j;
       if (dl >= a.D) break;
+      if (FUSE) {
+#pragma unroll
+        for (int o = 0; o < TH; o += 2) {
+          const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{sr[o], sr[o + 1]};
+          const f32x2 r = f32x2{1.0f, 1.0f} - f32x2{vmax(e.x, -1.0f), vmax(e.y, -1.0f)};
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const float cc = r[h];
+            wv1[o + h] = vmed3(wv0[o + h], wv1[o + h], cc);  // second smallest
+            wi0[o + h] = cc < wv0[o + h] ? dl : wi0[o + h];
+            wv0[o + h] = vmin(wv0[o + h], cc);
+          }
+        }
+        continue;
+      }
       // buffer stores: the level plane as a buffer resource (scalar), the lane's
       // byte offset fixed for the tile, the row offset scalar -- no address VALU
       const __amdgpu_buffer_rsrc_t rs =
@@ -307,8 +360,7 @@ __global__ __launch_bounds__(NW * 64) void k_ncc_volume(const uint2* __restrict_
 #pragma unroll
     for (int o = 0; o < TH; o++) sr[o] = __int_as_float(0x7fc00000);
     for (int c = 0; c < a.nch; c++) store(c);
-    return;
-  }
+  } else {
   stage(0, 0, 0);
   // reference: packed rows y0-R .. y0+TH+R-1 in registers; its centred window
   // sums Sr' and 1/sqrt(var_r) from them (dot4 with ones / with itself)
@@ -393,6 +445,49 @@ __global__ __launch_bounds__(NW * 64) void k_ncc_volume(const uint2* __restrict_
     __syncthreads();  // step t+1's bands landed (vmcnt 0); this buffer free for t+2
   }
   store(c - 1);
+  }
+  if (FUSE) {
+    // merge the NW waves' partials of each of the tile's 64 x TH pixels; the
+    // band buffers are free (every wave passed the loop's last barrier)
+    constexpr int TP = TH * 64;
+    float* m0 = (float*)smem;
+    float* m1 = m0 + NW * TP;
+    int* mi = (int*)(m1 + NW * TP);
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < TH; o++) {
+      m0[wave * TP + o * 64 + lane] = wv0[o];
+      m1[wave * TP + o * 64 + lane] = wv1[o];
+      mi[wave * TP + o * 64 + lane] = wi0[o];
+    }
+    __syncthreads();
+    for (int q = tid; q < TP; q += NW * 64) {
+      const int xx = x0 + (q & 63), yy = y0 + (q >> 6);
+      float bv = m0[q];
+      int bi = mi[q];
+#pragma unroll
+      for (int w = 1; w < NW; w++) {
+        const float v = m0[w * TP + q];
+        const int i = mi[w * TP + q];
+        if (v < bv || (v == bv && i >= 0 && i < bi)) {
+          bv = v;
+          bi = i;
+        }
+      }
+      float c2 = kWtaInit;
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        const int i = mi[w * TP + q];
+        const float v = (i >= bi - 1 && i <= bi + 1) ? m1[w * TP + q] : m0[w * TP + q];
+        c2 = vmin(c2, v);
+      }
+      if (xx < W && yy < H) {
+        const long p = (long)yy * W + xx;
+        wo.disp[p] = bi >= 0 ? wo.levels[bi] : 0.0f;
+        if (wo.conf) wo.conf[p] = (bi < 0 || c2 == kWtaInit) ? 0.0f : c2 - bv;
+      }
+    }
+  }
 }
 
 // Host side: the chunk/level shift plan (every roundf of the definition is
@@ -458,26 +553,27 @@ NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const fl
 
 template <int K, int TH, int DPW, int NW, int BW, bool EVEN>
 int launch_ncc_bw(hipStream_t s, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
-                  size_t lds) {
+                  const WtaOut& wo, size_t lds) {
   constexpr int DC = NW * DPW;
   a.tiles_x = (a.W + 63) / 64;
   a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);
   a.tiles_per_xcd = (a.ntiles + 7) / 8;
   a.nch = (a.D + DC - 1) / DC;
   dim3 g(8 * a.tiles_per_xcd);
-  auto kern = k_ncc_volume<K, TH, DPW, NW, BW, EVEN>;
+  auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, EVEN, false> : k_ncc_volume<K, TH, DPW, NW, BW, EVEN, true>;
+  if (!vol) lds = std::max(lds, (size_t)3 * 4 * NW * TH * 64);  // the waves' WTA partials
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(ncc lds)");
-  hipLaunchKernelGGL(kern, g, dim3(NW * 64), lds, s, stats, pk, plan, a, vol);
-  MVS_LAUNCH_CHECK("k_ncc_volume");
+  hipLaunchKernelGGL(kern, g, dim3(NW * 64), lds, s, stats, pk, plan, a, vol, wo);
+  MVS_LAUNCH_CHECK(vol ? "k_ncc_volume" : "k_ncc_volume (fused WTA)");
   return 0;
 }
 
 // returns 1 if this variant does not fit the LDS (caller tries a smaller one)
 template <int K, int TH, int DPW, int NW>
 int launch_ncc_t(mvs_ctx* ctx, const uint2* stats, const uint2* pk, NccArgs& a, const float* levels_host,
-                 const float* fdx, const float* fdy, float bl, float* vol, size_t lds_cap) {
+                 const float* fdx, const float* fdy, float bl, float* vol, const WtaOut& wo, size_t lds_cap) {
   NccPlan p = make_plan<K, TH, DPW, NW>(levels_host, a.D, a.nn, fdx, fdy, bl);
   const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * p.band_w;
   if (lds > lds_cap || p.band_w > 256) return 1;
@@ -488,13 +584,13 @@ int launch_ncc_t(mvs_ctx* ctx, const uint2* stats, const uint2* pk, NccArgs& a, 
   a.st_pairs = p.st_pairs;
   const NccRec* plan = (const NccRec*)dev;
   if (p.even) {
-    if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, NW, 128, true>(ctx->stream, stats, pk, plan, a, vol, lds);
-    if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, NW, 192, true>(ctx->stream, stats, pk, plan, a, vol, lds);
-    return launch_ncc_bw<K, TH, DPW, NW, 256, true>(ctx->stream, stats, pk, plan, a, vol, lds);
+    if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, NW, 128, true>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
+    if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, NW, 192, true>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
+    return launch_ncc_bw<K, TH, DPW, NW, 256, true>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
   }
-  if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, NW, 128, false>(ctx->stream, stats, pk, plan, a, vol, lds);
-  if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, NW, 192, false>(ctx->stream, stats, pk, plan, a, vol, lds);
-  return launch_ncc_bw<K, TH, DPW, NW, 256, false>(ctx->stream, stats, pk, plan, a, vol, lds);
+  if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, NW, 128, false>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
+  if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, NW, 192, false>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
+  return launch_ncc_bw<K, TH, DPW, NW, 256, false>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
 }
 
 }  // namespace
@@ -513,7 +609,10 @@ int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int 
 }
 
 int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
-                      const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol) {
+                      const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol,
+                      const float* levels_dev, float* disp, float* conf) {
+  if (!vol && (!levels_dev || !disp)) return arg_fail("fused NCC sweep needs levels and disp");
+  const WtaOut wo{levels_dev, disp, conf};
   if (W < 2) return arg_fail("NCC sweep needs W >= 2");
   NccArgs a{};
   a.W = W; a.H = H; a.D = D; a.z = z;
@@ -544,7 +643,7 @@ int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, con
   // workgroups per CU (vertical shifts grow the bands: fewer levels per step
   // then beat a single resident workgroup), then any that fits the LDS
 #define MVS_NCC_TRY(KK, DD, WW)                                                                     \
-  if (rc == 1) rc = launch_ncc_t<KK, 8, DD, WW>(ctx, stats, pk, a, levels_host, fdx, fdy, bl, vol, cap);
+  if (rc == 1) rc = launch_ncc_t<KK, 8, DD, WW>(ctx, stats, pk, a, levels_host, fdx, fdy, bl, vol, wo, cap);
   for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
     if (K == 5) {
       if (nw_env >= 8 && dpw_env >= 4) MVS_NCC_TRY(5, 4, 8)

@@ -171,6 +171,17 @@ class Engine:
                    "mvs_ncc_volume_d")
         return out
 
+    def ncc_wta(self, l8, box, cam: CameraArray, z: int, K: int = 5, disp=None, conf=None, want_conf: bool = True):
+        """ncc_volume + wta in one kernel: the volume never reaches HBM (bit-identical)."""
+        V, H, W = l8.shape
+        disp = self.empty((H, W), torch.float32) if disp is None else disp
+        if want_conf and conf is None:
+            conf = self.empty((H, W), torch.float32)
+        self._stream()
+        _lib.check(self.L.mvs_ncc_wta_d(self.ctx, W, H, _ptr(l8), _ptr(box), cam.desc(), K, z, _ptr(disp),
+                                        _ptr(conf) if want_conf else None), "mvs_ncc_wta_d")
+        return disp, conf
+
     def levels_dev(self, cam: CameraArray) -> torch.Tensor:
         key = cam.levels.tobytes()
         t = self._levels_dev.get(key)

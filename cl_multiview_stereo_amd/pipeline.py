@@ -59,13 +59,16 @@ class PhotoConsistency:
 class PixelSweep:
     """Per-pixel plane sweep.  cost="ncc": build-defined KxK NCC cost volume
     [D][H][W] per reference view, then WTA + confidence (the HBM-streaming
-    pass).  cost="sad": the reference sweep at S=1 grid semantics (parity)."""
+    pass); fused=True folds the WTA into the sweep kernel (mvs_ncc_wta_d: no
+    volume in HBM, same disp/conf bits).  cost="sad": the reference sweep at
+    S=1 grid semantics (parity)."""
 
-    def __init__(self, engine: Engine, cam: CameraArray, W: int, H: int, cost: str = "ncc", window: int = 5):
+    def __init__(self, engine: Engine, cam: CameraArray, W: int, H: int, cost: str = "ncc", window: int = 5,
+                 fused: bool = False):
         self.e, self.cam, self.W, self.H = engine, cam, W, H
-        self.cost, self.K = cost, window
+        self.cost, self.K, self.fused = cost, window, fused
         self.vol = None
-        if cost == "ncc":
+        if cost == "ncc" and not fused:
             self.vol = engine.empty((cam.D, H, W), torch.float32)
         self.levels = engine.levels_dev(cam)
 
@@ -79,6 +82,9 @@ class PixelSweep:
         conf = self.e.empty((n, self.H, self.W), torch.float32) if conf_out is None else conf_out
         box = self.e.box_stats(l8, self.K)
         for i, z in enumerate(range(z0, z1)):
+            if self.fused:
+                self.e.ncc_wta(l8, box, self.cam, z, self.K, disp=disp[i], conf=conf[i])
+                continue
             self.e.ncc_volume(l8, box, self.cam, z, self.K, out=self.vol)
             self.e.wta(self.vol, self.levels, disp=disp[i], conf=conf[i])
         return disp, conf
@@ -134,7 +140,7 @@ class Pipeline:
 
     def __init__(self, engine: Engine, settings: params.Settings, W: int, H: int,
                  view_subset: list[list[int]] | None = None, pixel_cost: str | None = "ncc",
-                 refine: bool = False, filt: bool = False, concurrent: bool = False):
+                 refine: bool = False, filt: bool = False, concurrent: bool = False, fused: bool = False):
         self.e, self.st, self.W, self.H = engine, settings, W, H
         vs = view_subset if view_subset is not None else params.neighbour_lists(
             settings.array_width, settings.array_height, settings.neib_hor, settings.neib_ver)
@@ -143,7 +149,7 @@ class Pipeline:
         self.cam = CameraArray(settings.array_width, settings.bl_ratio, levels, mat, num)
         self.slic = SLIC(engine, settings)
         self.photo = PhotoConsistency(engine, self.cam, settings.spixl_size)
-        self.pixel = PixelSweep(engine, self.cam, W, H, pixel_cost, settings.window) if pixel_cost else None
+        self.pixel = PixelSweep(engine, self.cam, W, H, pixel_cost, settings.window, fused) if pixel_cost else None
         self.refiner = DepthRefinement(engine, self.cam, settings.spixl_size) if refine else None
         self.filter = ConsistencyFilter(engine, settings.array_width, settings.bl_ratio, settings.fuse) if filt else None
         self.side = None

@@ -131,6 +131,11 @@ int mvs_ncc_volume_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_
 /* Winner-take-all over vol [D][H][W]: disp = levels[first argmin], conf =
  * (min cost outside best+-1) - best cost.  conf may be NULL. */
 int mvs_wta_d(mvs_ctx* ctx, int W, int H, int D, const float* vol, const float* levels, float* disp, float* conf);
+/* mvs_ncc_volume_d + mvs_wta_d fused: the cost volume never reaches HBM.
+ * disp/conf [H][W] are bit-identical to the two-pass result (levels from a->levels);
+ * conf may be NULL. */
+int mvs_ncc_wta_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
+                  int K, int z, float* disp, float* conf);
 
 /* Superpixel-plane refinement (clDepthRefinement, depth_refinement.cpp:91-1470).
  * flat [V][mh][mw][2] and state/state2 [V][mh][mw][6] are caller-provided

@@ -57,6 +57,11 @@ def main():
     if run("ncc"):
         out["ncc_volume_1view"] = timeit(lambda: e.ncc_volume(l8, box, cam, 2, 5, out=vol))
         out["ncc_volume_view0"] = timeit(lambda: e.ncc_volume(l8, box, cam, 0, 5, out=vol))
+    if run("fused"):  # sweep + WTA in one kernel, no volume
+        d1, c1 = e.ncc_wta(l8, box, cam, 2, 5)
+        out["ncc_wta_fused_1view"] = timeit(lambda: e.ncc_wta(l8, box, cam, 2, 5, disp=d1, conf=c1))
+        out["ncc_wta_fused_view0"] = timeit(lambda: e.ncc_wta(l8, box, cam, 0, 5, disp=d1, conf=c1))
+        out["ncc_then_wta_1view"] = timeit(lambda: (e.ncc_volume(l8, box, cam, 2, 5, out=vol), e.wta(vol, lv)))
     if run("fill"):  # write floor: one pass of stores over a cost volume
         out["fill_volume"] = timeit(lambda: vol.fill_(1.0))
     if run("wta"):

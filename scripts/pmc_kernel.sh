@@ -11,7 +11,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
            "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr"; do
   i=$((i+1))
-  timeout -s KILL 200 rocprofv3 --pmc $grp --kernel-include-regex "${KERNEL:-k_propagate}" -d $OUT/p$i -o run -- python3 bench.py --config ${CONFIG:-ref} --steps 1 --warmup 0 --no-cpu-baseline > $OUT/p$i.txt 2>&1 || echo "pass $i failed rc=$?"
+  timeout -s KILL 200 rocprofv3 --pmc $grp --kernel-include-regex "${KERNEL:-k_propagate}" -d $OUT/p$i -o run -- python3 bench.py --config ${CONFIG:-ref} --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_EXTRA:-} > $OUT/p$i.txt 2>&1 || echo "pass $i failed rc=$?"
 done
 python3 - <<'PY'
 import sqlite3, glob, collections

@@ -72,7 +72,8 @@ def main():
     ncc = [k for k in sorted(pmc) if k.startswith("k_ncc_volume") and "SQ_INSTS_VALU_per_launch" in pmc[k]]
     if ncc:
         json.dump({k: {"valu_wave_insts_per_launch": pmc[k]["SQ_INSTS_VALU_per_launch"],
-                       "lds_wave_insts_per_launch": pmc[k].get("SQ_INSTS_LDS_per_launch")} for k in ncc} |
+                       "lds_wave_insts_per_launch": pmc[k].get("SQ_INSTS_LDS_per_launch"),
+                       "launches": pmc[k]["launches"]} for k in ncc} |
                   {"source": f"profiles/{tag}_pmc.json", "note": "SQ_INSTS_VALU / SQ_INSTS_LDS, own --pmc pass"},
                   open(os.path.join(out, "pmc_ncc.json"), "w"), indent=1)
     for r in rows[:8]:

@@ -151,6 +151,40 @@ def test_ncc_volume_and_wta(engine, name, K):
         od, oc = orc.wta(want, b["levels"])
         assert_bits(disp.cpu().numpy(), od, "wta disp")
         assert_bits(conf.cpu().numpy(), oc, "wta conf")
+        fd, fc = engine.ncc_wta(l8, box, cam, z, K)  # fused: no volume
+        assert_bits(fd.cpu().numpy(), od, "fused wta disp")
+        assert_bits(fc.cpu().numpy(), oc, "fused wta conf")
+
+
+@pytest.mark.parametrize("name,dmax,flat", [("d1", 0, False), ("d2", 1, False), ("d3", 2, True), ("d5", 4, False),
+                                            ("d9_flat", 8, True), ("d33_flat", 32, True), ("d70", 69, False)])
+def test_ncc_wta_fused_edges(engine, name, dmax, flat):
+    """Fused sweep+WTA vs the oracle's volume + WTA at level counts below /
+    around the NW=8 waves x DPW=4 chunk, and with textureless (constant)
+    patches, whose cost ties (cost 1 at every level) exercise the first-argmin
+    tie rule across waves.  View 0 of a 3x1 array with no neighbours listed
+    exercises the every-window-invalid path."""
+    c = dict(aw=3, ah=1, W=133, H=29, dmin=0, dmax=dmax, bl=1.0, nh=2, nv=0, seed=37)
+    b = build(c)
+    stack = b["stack"].copy()
+    if flat:
+        stack[:, 5:20, 10:70, :3] = 128
+        stack[1, :, 90:120, :3] = 40
+    sn = b["sn"].copy()
+    sn[0] = 0
+    lab, l8 = engine.cvt(dev(stack))
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], sn)
+    l8h = l8.cpu().numpy()
+    for K in (5, 7):
+        box = engine.box_stats(l8, K)
+        for z in range(b["V"]):
+            want = orc.ncc_volume(l8h, b["levels"], b["vs"], sn, c["aw"], c["bl"], K, z)
+            od, oc = orc.wta(want, b["levels"])
+            fd, fc = engine.ncc_wta(l8, box, cam, z, K)
+            assert_bits(fd.cpu().numpy(), od, f"fused disp K{K} z{z}")
+            assert_bits(fc.cpu().numpy(), oc, f"fused conf K{K} z{z}")
+            fd2, _ = engine.ncc_wta(l8, box, cam, z, K, want_conf=False)
+            assert_bits(fd2.cpu().numpy(), od, f"fused disp (no conf) K{K} z{z}")
 
 
 @pytest.mark.parametrize("name,ks,kst", [("c3x3_s8", 26, 13), ("c3x1_s16", 52, 13), ("c5x1_s32", 1080, 13),

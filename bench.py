@@ -103,7 +103,7 @@ def main():
                     filt=bool(cfg.get("filt")) and not sharded, concurrent=args.concurrent, fused=args.fused)
     if sharded:
         from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
-        spipe = ShardedPipeline(EngineBackend(e), st, pipe.cam, ViewGather(V), pixel_cost=cost, refine=True,
+        spipe = ShardedPipeline(EngineBackend(e, fused=args.fused), st, pipe.cam, ViewGather(V), pixel_cost=cost, refine=True,
                                 filt=bool(cfg.get("filt")))
 
     # HIP events around the cost-volume kernels, on the stream they run on

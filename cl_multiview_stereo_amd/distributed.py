@@ -166,10 +166,11 @@ class ShardedPipeline:
 
 
 class EngineBackend:
-    """Per-rank compute on the GPU through libmvs.so (Engine)."""
+    """Per-rank compute on the GPU through libmvs.so (Engine).  fused: the per-pixel
+    NCC sweep folds its winner-take-all in (no cost volume; same maps)."""
 
-    def __init__(self, engine):
-        self.e = engine
+    def __init__(self, engine, fused: bool = False):
+        self.e, self.fused = engine, fused
         self._sweeps = {}  # PixelSweep (volume buffers, side stream) per configuration
 
     def cvt(self, rgbx):
@@ -192,7 +193,7 @@ class EngineBackend:
         key = (id(cam), W, H, cost, K)
         ps = self._sweeps.get(key)
         if ps is None:
-            ps = self._sweeps[key] = PixelSweep(self.e, cam, W, H, cost, K)
+            ps = self._sweeps[key] = PixelSweep(self.e, cam, W, H, cost, K, self.fused)
         return ps.run(lab, l8, z0, z1)
 
     def flatness(self, spixl, gamma):

@@ -332,7 +332,8 @@ def test_slic_ties(engine, kind):
 @pytest.mark.parametrize("name", ["c3x1_s16", "c3x3_s8"])
 def test_concurrent_pipeline_matches_serial(engine, name):
     """Pipeline(concurrent=True) runs the superpixel chain on a second stream
-    and context: every output equals the one-stream pipeline's bit for bit."""
+    and context, fused=True folds the WTA into the sweep: every output equals
+    the one-stream two-pass pipeline's bit for bit."""
     from cl_multiview_stereo_amd.pipeline import Pipeline
     c = CASES[name]
     b = build(c)
@@ -341,11 +342,12 @@ def test_concurrent_pipeline_matches_serial(engine, name):
                          cost="ncc")
     rgbx = dev(b["stack"])
     outs = []
-    for conc in (False, True):
-        p = Pipeline(engine, st, c["W"], c["H"], concurrent=conc)
+    for conc, fused in ((False, False), (True, False), (False, True), (True, True)):
+        p = Pipeline(engine, st, c["W"], c["H"], concurrent=conc, fused=fused)
         o = p.exe_pipeline(rgbx)
         o = p.exe_pipeline(rgbx)  # twice: the second run reuses cached allocator blocks across streams
         torch.cuda.synchronize()
         outs.append(o)
-    for f in ("spixl", "labels", "rep", "disp", "conf"):
-        assert_bits(getattr(outs[1], f).cpu().numpy(), getattr(outs[0], f).cpu().numpy(), f)
+    for o in outs[1:]:
+        for f in ("spixl", "labels", "rep", "disp", "conf"):
+            assert_bits(getattr(o, f).cpu().numpy(), getattr(outs[0], f).cpu().numpy(), f)

@@ -119,20 +119,21 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       float fdy = (a.bl * d) * (float)(vy - ry);
       const float4* labv = lab + (long)view * P;
       float val = 0.0f;
+      // branch-free taps: every load is issued (out-of-image taps read pixel 0
+      // and are dropped by the select), so the 25 gathers of a neighbour are
+      // independent and in flight together instead of one per branch
 #pragma unroll 5
       for (int t = 0; t < 25; t++) {
         int2 r = refxy[w][t];
         int xp = (int)((float)r.x - fdx);
         int yp = (int)((float)r.y - fdy);
-        val = val + 30.0f;
-        if (r.x >= 0 && r.y >= 0 && xp >= 0 && yp >= 0 && r.x < a.W && r.y < a.H && xp < a.W && yp < a.H) {
-          val = val - 30.0f;
-          float4 A = refc[w][t];
-          float4 B = labv[(long)yp * a.W + xp];
-          float ad = fabsf(A.x - B.x) + fabsf(A.y - B.y);
-          ad = ad + fabsf(A.z - B.z);
-          val = val + ad;
-        }
+        const bool in = r.x >= 0 && r.y >= 0 && xp >= 0 && yp >= 0 && r.x < a.W && r.y < a.H && xp < a.W && yp < a.H;
+        const float4 B = labv[in ? yp * a.W + xp : 0];
+        const float4 A = refc[w][t];
+        float ad = fabsf(A.x - B.x) + fabsf(A.y - B.y);
+        ad = ad + fabsf(A.z - B.z);
+        const float v30 = val + 30.0f;  // the reference's val += 30; val -= 30; val += AD
+        val = in ? (v30 - 30.0f) + ad : v30;
       }
       if (val < mn) mn = val;
     }

@@ -125,6 +125,20 @@ def test_grid_and_pixel_sad(engine, name):
     assert_bits(sp.cpu().numpy()[..., 7], want, "grid sweep == per-pixel sweep")
 
 
+def test_cvt_every_rgb_colour(engine):
+    """k_cvt on all 2^24 8-bit colours (one 4096x4096 RGBx image) against the
+    oracle: the cube-root fast path (slic.hip powr_third) must round exactly as
+    the definition mvs_powrf does, and the 8-bit NCC intensity follows L."""
+    v = np.arange(1 << 24, dtype=np.uint32)
+    rgbx = np.zeros((1, 4096, 4096, 4), np.uint8)
+    flat = rgbx[0].reshape(-1, 4)
+    flat[:, 0], flat[:, 1], flat[:, 2] = v & 255, (v >> 8) & 255, v >> 16
+    lab, l8 = engine.cvt(dev(rgbx))
+    want = orc.cvt(rgbx)
+    assert_bits(lab.cpu().numpy(), want, "Lab of every colour")
+    assert_bits(l8.cpu().numpy(), orc.l8(want), "l8 of every colour")
+
+
 @pytest.mark.parametrize("K", [5, 7])
 @pytest.mark.parametrize("name", ["c2x1_pix", "c2x2_pix", "c3x1_pix_odd", "c5x1_ncc", "c4x1_ncc_d40", "c3x1_inc3"])
 def test_ncc_volume_and_wta(engine, name, K):

@@ -473,149 +473,198 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     return x < c.mw - off - 1 ? M * z + (long)c.mw * y + (x + off + 1) : -1;
   };
   const int nslot = 9 + 4 * nks;
-  for (int b = 0; b < nslot; b += 64) {
-    const int k = b + lane;
-    const long q = k < nslot ? cand(k) : -1;
-    float di = 0.f, sm1 = 0.f, cs1 = 0.f, simi = 0.f, nx = 0.f, ny = 0.f, nz = 1.f;
-    if (q >= 0) {  // update(), clcode.cl:1635-1673, minus the accept test
-      const float* s1 = st_in + 6 * q;
-      nx = s1[3]; ny = s1[4]; nz = s1[5];
-      const float* sc = spixl + 8 * q;
-      float t = nx * (sc[1] - p.cx);
-      t = t + ny * (sc[2] - p.cy);
-      t = t + nz * s1[0];
-      di = t / nz;
-      sm1 = smooth(di, nx, ny, nz);
-      cs1 = comp_consistency(p, di, nx, ny, nz);
-      const float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], sc[3], sc[4], sc[5]);
-      simi = expf_neg_sq(diff, c.gamma);
-    }
-    const unsigned long long valid = __ballot(q >= 0);
-    for (int l = 0; l < 64 && b + l < nslot; l++) {  // accept tests in order, on every lane
-      if (!((valid >> l) & 1ull)) continue;
-      const float ksm = bcast(sm1, l), kcs = bcast(cs1, l), ksi = bcast(simi, l);
-      if ((iter < 4 && ksm * ksi > cur.sm) || kcs * ksm > cur.sm * cur.cs) {
-        cur.d = bcast(di, l); cur.sm = ksm; cur.cs = kcs;
-        cur.nx = bcast(nx, l); cur.ny = bcast(ny, l); cur.nz = bcast(nz, l);
-      }
-    }
-  }
-
-  // spatialRefinement over the 8 neighbour triangles (clcode.cl:1676-1723, 1808-1820).
-  // Lane-parallel form (fast smoothness terms, <= kTriViews views): lane 8t+r
-  // works for triangle t.  The smoothness products simi_l * exp(...) are
-  // computed by lanes r = l mod 8 into LDS and summed in term order by lane 8t;
-  // each view's consistency sums (9 samples in order) by lane r = view mod 8,
-  // combined in view order by lane 8t -- every float sum in the reference's
-  // order, so bit-identical to the one-lane-per-triangle form kept below.
   const int nv = sn[z];
   if (fast_sm && nv <= kTriViews) {
+    // Lane-parallel evaluation in groups of 8 candidates: lane 8t + r works
+    // for candidate t of the group.  The smoothness products simi_l * exp(...)
+    // are computed by lanes r = l mod 8 into LDS and summed in term order by
+    // lane 8t; each view's consistency sums (9 samples in order) by lane
+    // r = view mod 8, combined in view order by lane 8t -- every float sum in
+    // the reference's order, so bit-identical to the one-lane-per-candidate
+    // forms kept below.  Groups: the valid plane candidates (compacted, slot
+    // order), then the 8 spatial-refinement triangles (clcode.cl:1676-1723,
+    // 1808-1820), whose normals use the depth after every plane candidate.
+    // At S = 8 most far candidates leave the map, so one group of 8 neighbour
+    // planes keeps all 64 lanes busy instead of 8.
     __shared__ float s_prod[4][8][64];
     __shared__ float s_view[4][8][kTriViews][5];
+    __shared__ int s_slot[4][64];
     const int w = threadIdx.x >> 6;
     const int t = lane >> 3, r = lane & 7;
-    const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
-    const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
-    const int u = (t + 1) % 8;
-    const bool ok = nbx[t] > -1 && nby[t] > -1 && nbx[t] < c.mw && nby[t] < c.mh && nbx[u] > -1 && nby[u] > -1 &&
-                    nbx[u] < c.mw && nby[u] < c.mh;
-    float n0 = 0.f, n1 = 0.f, n2 = 0.f;
-    if (ok) {
-      const long q1 = M * z + (long)c.mw * nby[t] + nbx[t], q2 = M * z + (long)c.mw * nby[u] + nbx[u];
-      const float* a1 = spixl + 8 * q1;
-      const float* a2 = spixl + 8 * q2;
-      const float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = st_in[6 * q1] - cur.d;
-      const float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = st_in[6 * q2] - cur.d;
-      n0 = v1y * v2z - v1z * v2y;
-      n1 = v2x * v1z - v1x * v2z;
-      n2 = v1x * v2y - v1y * v2x;
-      float ss = n0 * n0;
-      ss = ss + n1 * n1;
-      ss = ss + n2 * n2;
-      ss = ss + 0.0f * 0.0f;
-      if (ss != 0.0f) {
-        const float rr = sqrtf(ss);
-        n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
-      }
-    }
-    const float rn2 = 1.0f / n2;
-    // smoothness products; uniform trip count so every lane takes part in the shuffles
-    for (int i = 0; i < (nterm + 7) / 8; i++) {
-      const int l = r + 8 * i;
-      const int ls = l < 64 ? l : 0;
-      const float simi = __shfl(t_simi, ls), sx = __shfl(t_sx, ls), sy = __shfl(t_sy, ls), sd = __shfl(t_sd, ls);
-      if (ok && l < nterm && ((t_valid >> l) & 1ull)) {
-        const float di = plane_at_r(n0, n1, n2, rn2, p.cx, p.cy, cur.d, sx, sy);
-        const float diff = di - sd;
-        s_prod[w][t][l] = simi * expf_neg_sq(diff, c.alpha);
-      }
-    }
-    for (int k = r; k < nv; k += 8)
-      if (ok) view_sums(p, cur.d, n0, n1, n2, k, s_view[w][t][k]);
+    const long qk = lane < nslot ? cand(lane) : -1;
+    const unsigned long long vmask = __ballot(qk >= 0);
+    if (qk >= 0) s_slot[w][__popcll(vmask & ((1ull << lane) - 1ull))] = lane;
+    const int nvalid = __popcll(vmask);
+    const int ngrp = (nvalid + 7) / 8;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float sm1 = 0.f, cs1 = 0.f;
-    if (ok && r == 0) {
-      float sm = 0.0f;
-      for (int l = 0; l < nterm; l++)
-        if ((t_valid >> l) & 1ull) sm = sm + s_prod[w][t][l];
-      sm1 = wn > 0 ? sm / wn : 0.000001f;
-      float cons = 0.0f;
-      int vc = 0;
-      for (int k = 0; k < nv; k++) {
-        const float* o = s_view[w][t][k];
-        const float num = o[0], vis_w = o[1], occ_w = o[2], visibility = o[3], visible = o[4];
-        if (num > 0) {
-          vc++;
-          if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
-          if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)p.fl.y);
+    const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
+    const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
+    for (int gi = 0; gi <= ngrp; gi++) {
+      const bool tri = gi == ngrp;
+      bool ok;
+      float pd = cur.d, n0 = 0.f, n1 = 0.f, n2 = 1.f, ksimi = 0.f;
+      if (!tri) {  // plane candidate: update(), clcode.cl:1635-1673, minus the accept test
+        const int j = gi * 8 + t;
+        ok = j < nvalid;
+        if (ok) {
+          const long q = cand(s_slot[w][j]);
+          const float* s1 = st_in + 6 * q;
+          n0 = s1[3]; n1 = s1[4]; n2 = s1[5];
+          const float* sc = spixl + 8 * q;
+          float tt = n0 * (sc[1] - p.cx);
+          tt = tt + n1 * (sc[2] - p.cy);
+          tt = tt + n2 * s1[0];
+          pd = tt / n2;
+          const float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], sc[3], sc[4], sc[5]);
+          ksimi = expf_neg_sq(diff, c.gamma);
+        }
+      } else {  // triangle t: normalize(cross(c_t - c, c_{t+1} - c)) at the current depth
+        const int u = (t + 1) % 8;
+        ok = nbx[t] > -1 && nby[t] > -1 && nbx[t] < c.mw && nby[t] < c.mh && nbx[u] > -1 && nby[u] > -1 &&
+             nbx[u] < c.mw && nby[u] < c.mh;
+        n2 = 0.f;
+        if (ok) {
+          const long q1 = M * z + (long)c.mw * nby[t] + nbx[t], q2 = M * z + (long)c.mw * nby[u] + nbx[u];
+          const float* a1 = spixl + 8 * q1;
+          const float* a2 = spixl + 8 * q2;
+          const float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = st_in[6 * q1] - cur.d;
+          const float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = st_in[6 * q2] - cur.d;
+          n0 = v1y * v2z - v1z * v2y;
+          n1 = v2x * v1z - v1x * v2z;
+          n2 = v1x * v2y - v1y * v2x;
+          float ss = n0 * n0;
+          ss = ss + n1 * n1;
+          ss = ss + n2 * n2;
+          ss = ss + 0.0f * 0.0f;
+          if (ss != 0.0f) {
+            const float rr = sqrtf(ss);
+            n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
+          }
         }
       }
-      cs1 = finish_consistency(cons, vc);
-    }
-    const unsigned long long valid = __ballot(ok && r == 0);
-    for (int l = 0; l < 8; l++) {
-      if (!((valid >> (8 * l)) & 1ull)) continue;
-      const float ksm = bcast(sm1, 8 * l), kcs = bcast(cs1, 8 * l);
-      if ((iter < 4 && ksm > cur.sm) || ksm * kcs > cur.sm * cur.cs) {
-        cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, 8 * l); cur.ny = bcast(n1, 8 * l); cur.nz = bcast(n2, 8 * l);
+      const float rn2 = 1.0f / n2;
+      // smoothness products; uniform trip count so every lane takes part in the shuffles
+      for (int i = 0; i < (nterm + 7) / 8; i++) {
+        const int l = r + 8 * i;
+        const int ls = l < 64 ? l : 0;
+        const float simi = __shfl(t_simi, ls), sx = __shfl(t_sx, ls), sy = __shfl(t_sy, ls), sd = __shfl(t_sd, ls);
+        if (ok && l < nterm && ((t_valid >> l) & 1ull)) {
+          const float di = plane_at_r(n0, n1, n2, rn2, p.cx, p.cy, pd, sx, sy);
+          const float diff = di - sd;
+          s_prod[w][t][l] = simi * expf_neg_sq(diff, c.alpha);
+        }
+      }
+      for (int k = r; k < nv; k += 8)
+        if (ok) view_sums(p, pd, n0, n1, n2, k, s_view[w][t][k]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float sm1 = 0.f, cs1 = 0.f;
+      if (ok && r == 0) {
+        float sm = 0.0f;
+        for (int l = 0; l < nterm; l++)
+          if ((t_valid >> l) & 1ull) sm = sm + s_prod[w][t][l];
+        sm1 = wn > 0 ? sm / wn : 0.000001f;
+        float cons = 0.0f;
+        int vc = 0;
+        for (int k = 0; k < nv; k++) {
+          const float* o = s_view[w][t][k];
+          const float num = o[0], vis_w = o[1], occ_w = o[2], visibility = o[3], visible = o[4];
+          if (num > 0) {
+            vc++;
+            if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+            if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)p.fl.y);
+          }
+        }
+        cs1 = finish_consistency(cons, vc);
+      }
+      // lane 8t's reads of this group's LDS sums are done before the next group writes
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const unsigned long long valid = __ballot(ok && r == 0);
+      for (int l = 0; l < 8; l++) {  // accept tests in candidate order
+        if (!((valid >> (8 * l)) & 1ull)) continue;
+        const float ksm = bcast(sm1, 8 * l), kcs = bcast(cs1, 8 * l);
+        if (!tri) {
+          const float ksi = bcast(ksimi, 8 * l);
+          if ((iter < 4 && ksm * ksi > cur.sm) || kcs * ksm > cur.sm * cur.cs) {
+            cur.d = bcast(pd, 8 * l); cur.sm = ksm; cur.cs = kcs;
+            cur.nx = bcast(n0, 8 * l); cur.ny = bcast(n1, 8 * l); cur.nz = bcast(n2, 8 * l);
+          }
+        } else if ((iter < 4 && ksm > cur.sm) || ksm * kcs > cur.sm * cur.cs) {
+          cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, 8 * l); cur.ny = bcast(n1, 8 * l); cur.nz = bcast(n2, 8 * l);
+        }
       }
     }
   } else {
-    const int t = lane & 7;
-    const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
-    const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
-    const int u = (t + 1) % 8;
-    const bool ok = lane < 8 && nbx[t] > -1 && nby[t] > -1 && nbx[t] < c.mw && nby[t] < c.mh && nbx[u] > -1 &&
-                    nby[u] > -1 && nbx[u] < c.mw && nby[u] < c.mh;
-    float sm1 = 0.f, cs1 = 0.f, n0 = 0.f, n1 = 0.f, n2 = 0.f;
-    if (ok) {
-      const long q1 = M * z + (long)c.mw * nby[t] + nbx[t], q2 = M * z + (long)c.mw * nby[u] + nbx[u];
-      const float* a1 = spixl + 8 * q1;
-      const float* a2 = spixl + 8 * q2;
-      const float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = st_in[6 * q1] - cur.d;
-      const float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = st_in[6 * q2] - cur.d;
-      n0 = v1y * v2z - v1z * v2y;
-      n1 = v2x * v1z - v1x * v2z;
-      n2 = v1x * v2y - v1y * v2x;
-      float ss = n0 * n0;
-      ss = ss + n1 * n1;
-      ss = ss + n2 * n2;
-      ss = ss + 0.0f * 0.0f;
-      if (ss != 0.0f) {
-        const float rr = sqrtf(ss);
-        n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
+    // one lane per plane candidate, in batches of 64
+    for (int b = 0; b < nslot; b += 64) {
+      const int k = b + lane;
+      const long q = k < nslot ? cand(k) : -1;
+      float di = 0.f, sm1 = 0.f, cs1 = 0.f, simi = 0.f, nx = 0.f, ny = 0.f, nz = 1.f;
+      if (q >= 0) {  // update(), clcode.cl:1635-1673, minus the accept test
+        const float* s1 = st_in + 6 * q;
+        nx = s1[3]; ny = s1[4]; nz = s1[5];
+        const float* sc = spixl + 8 * q;
+        float t = nx * (sc[1] - p.cx);
+        t = t + ny * (sc[2] - p.cy);
+        t = t + nz * s1[0];
+        di = t / nz;
+        sm1 = smooth(di, nx, ny, nz);
+        cs1 = comp_consistency(p, di, nx, ny, nz);
+        const float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], sc[3], sc[4], sc[5]);
+        simi = expf_neg_sq(diff, c.gamma);
       }
-      sm1 = smooth(cur.d, n0, n1, n2);
-      cs1 = comp_consistency(p, cur.d, n0, n1, n2);
+      const unsigned long long valid = __ballot(q >= 0);
+      for (int l = 0; l < 64 && b + l < nslot; l++) {  // accept tests in order, on every lane
+        if (!((valid >> l) & 1ull)) continue;
+        const float ksm = bcast(sm1, l), kcs = bcast(cs1, l), ksi = bcast(simi, l);
+        if ((iter < 4 && ksm * ksi > cur.sm) || kcs * ksm > cur.sm * cur.cs) {
+          cur.d = bcast(di, l); cur.sm = ksm; cur.cs = kcs;
+          cur.nx = bcast(nx, l); cur.ny = bcast(ny, l); cur.nz = bcast(nz, l);
+        }
+      }
     }
-    const unsigned long long valid = __ballot(ok);
-    for (int l = 0; l < 8; l++) {
-      if (!((valid >> l) & 1ull)) continue;
-      const float ksm = bcast(sm1, l), kcs = bcast(cs1, l);
-      if ((iter < 4 && ksm > cur.sm) || ksm * kcs > cur.sm * cur.cs) {
-        cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, l); cur.ny = bcast(n1, l); cur.nz = bcast(n2, l);
+
+    // spatialRefinement, one lane per triangle
+    {
+      const int t = lane & 7;
+      const int nbx[8] = {x - 1, x - 1, x, x + 1, x + 1, x + 1, x, x - 1};
+      const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
+      const int u = (t + 1) % 8;
+      const bool ok = lane < 8 && nbx[t] > -1 && nby[t] > -1 && nbx[t] < c.mw && nby[t] < c.mh && nbx[u] > -1 &&
+                      nby[u] > -1 && nbx[u] < c.mw && nby[u] < c.mh;
+      float sm1 = 0.f, cs1 = 0.f, n0 = 0.f, n1 = 0.f, n2 = 0.f;
+      if (ok) {
+        const long q1 = M * z + (long)c.mw * nby[t] + nbx[t], q2 = M * z + (long)c.mw * nby[u] + nbx[u];
+        const float* a1 = spixl + 8 * q1;
+        const float* a2 = spixl + 8 * q2;
+        const float v1x = a1[1] - p.cx, v1y = a1[2] - p.cy, v1z = st_in[6 * q1] - cur.d;
+        const float v2x = a2[1] - p.cx, v2y = a2[2] - p.cy, v2z = st_in[6 * q2] - cur.d;
+        n0 = v1y * v2z - v1z * v2y;
+        n1 = v2x * v1z - v1x * v2z;
+        n2 = v1x * v2y - v1y * v2x;
+        float ss = n0 * n0;
+        ss = ss + n1 * n1;
+        ss = ss + n2 * n2;
+        ss = ss + 0.0f * 0.0f;
+        if (ss != 0.0f) {
+          const float rr = sqrtf(ss);
+          n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
+        }
+        sm1 = smooth(cur.d, n0, n1, n2);
+        cs1 = comp_consistency(p, cur.d, n0, n1, n2);
+      }
+      const unsigned long long valid = __ballot(ok);
+      for (int l = 0; l < 8; l++) {
+        if (!((valid >> l) & 1ull)) continue;
+        const float ksm = bcast(sm1, l), kcs = bcast(cs1, l);
+        if ((iter < 4 && ksm > cur.sm) || ksm * kcs > cur.sm * cur.cs) {
+          cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, l); cur.ny = bcast(n1, l); cur.nz = bcast(n2, l);
+        }
       }
     }
   }

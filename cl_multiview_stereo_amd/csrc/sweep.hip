@@ -66,17 +66,22 @@ struct SweepArgs {
 // reference views of the call run in one launch (blockIdx.y), so the GPU is
 // filled even at a few thousand superpixels per view.  The per-wave first
 // minima are combined in (cost, index) lexicographic order -- the reference's
-// strict-< scan over levels in index order -- through LDS.
+// strict-< scan over levels in index order -- through LDS.  LPS = 32 (D <= 32,
+// e.g. the reference's default 31 levels): two superpixels per wave, one per
+// 32-lane half, so no lane idles past the last level.
+template <int LPS>
 __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ lab, float* __restrict__ spixl,
                                                      const uint8_t* __restrict__ rep,
                                                      const float* __restrict__ levels, const int* __restrict__ vs,
                                                      const int* __restrict__ sn, SweepArgs a, int wps) {
-  __shared__ float4 refc[4][25];
-  __shared__ int2 refxy[4][25];
+  __shared__ float4 refc[8][25];
+  __shared__ int2 refxy[8][25];
   __shared__ float wbest[4];
   __shared__ int wbi[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int spb = 4 / wps, h = w % wps;
+  const int ll = lane & (LPS - 1);                              // level lane within the superpixel's lanes
+  const int spb = LPS == 64 ? 4 / wps : 8, h = LPS == 64 ? w % wps : 0;
+  const int slot = LPS == 64 ? w / wps : 2 * w + (lane >> 5);  // superpixel of this block
   const int z = a.z + blockIdx.y;
   const long M = (long)a.mw * a.mh, P = (long)a.W * a.H;
   // XCD-aware order: blocks are dealt round-robin over the 8 XCDs; give each
@@ -84,8 +89,8 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
   // touch are shared within one L2 instead of being fetched by all eight
   const long nb = (M + spb - 1) / spb, per = (nb + 7) / 8;
   const long blk = (long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  const long s = blk * spb + w / wps;
-  const bool active = blk < nb && s < M && w / wps < spb;
+  const long s = blk * spb + slot;
+  const bool active = blk < nb && s < M && slot < spb;
   const long idx = z * M + (active ? s : 0);
   const uint8_t* dr = rep + 8 * idx;
   int bl_ = max((int)dr[0], max((int)dr[1], (int)dr[2]));
@@ -96,20 +101,20 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
   float sty = (float)fmax(1.0, 0.25 * (double)(float)(bt_ + bb_));
   float cx = spixl[8 * idx + 1], cy = spixl[8 * idx + 2];
   const float4* labz = lab + (long)z * P;
-  if (lane < 25) {
-    int i = lane / 5 - 2, j = lane % 5 - 2;  // tap order: i (x) outer, j (y) inner
+  if (ll < 25 && (LPS == 32 || h == 0)) {
+    int i = ll / 5 - 2, j = ll % 5 - 2;  // tap order: i (x) outer, j (y) inner
     int xr = (int)(cx + (float)i * stx);
     int yr = (int)(cy + (float)j * sty);
-    refxy[w][lane] = make_int2(xr, yr);
+    refxy[slot][ll] = make_int2(xr, yr);
     bool in = xr >= 0 && yr >= 0 && xr < a.W && yr < a.H;
-    refc[w][lane] = in ? labz[(long)yr * a.W + xr] : make_float4(0.f, 0.f, 0.f, 0.f);
+    refc[slot][ll] = in ? labz[(long)yr * a.W + xr] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
   int rx = z % a.aw, ry = z / a.aw;
   int nn = sn[z];
   float best = 1000000.0f;
   int bi = 0x7fffffff;
-  for (int dl = lane + 64 * h; dl < a.D; dl += 64 * wps) {
+  for (int dl = ll + LPS * h; dl < a.D; dl += LPS * wps) {
     float d = levels[dl];
     float mn = 1000000.0f;
     for (int n = 0; n < nn; n++) {
@@ -124,12 +129,12 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       // independent and in flight together instead of one per branch
 #pragma unroll 5
       for (int t = 0; t < 25; t++) {
-        int2 r = refxy[w][t];
+        int2 r = refxy[slot][t];
         int xp = (int)((float)r.x - fdx);
         int yp = (int)((float)r.y - fdy);
         const bool in = r.x >= 0 && r.y >= 0 && xp >= 0 && yp >= 0 && r.x < a.W && r.y < a.H && xp < a.W && yp < a.H;
         const float4 B = labv[in ? yp * a.W + xp : 0];
-        const float4 A = refc[w][t];
+        const float4 A = refc[slot][t];
         float ad = fabsf(A.x - B.x) + fabsf(A.y - B.y);
         ad = ad + fabsf(A.z - B.z);
         const float v30 = val + 30.0f;  // the reference's val += 30; val -= 30; val += AD
@@ -142,15 +147,19 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       bi = dl;
     }
   }
-  // first minimum across lanes: (cost, index) lexicographic
+  // first minimum across the superpixel's lanes: (cost, index) lexicographic
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
+  for (int o = LPS / 2; o >= 1; o >>= 1) {
     float ob = __shfl_xor(best, o, 64);
     int oi = __shfl_xor(bi, o, 64);
     if (ob < best || (ob == best && oi < bi)) {
       best = ob;
       bi = oi;
     }
+  }
+  if (LPS == 32) {
+    if (active && ll == 0) spixl[8 * idx + 7] = (bi != 0x7fffffff && best < 1000000.0f) ? levels[bi] : 0.0f;
+    return;
   }
   if (lane == 0) {
     wbest[w] = best;
@@ -348,11 +357,12 @@ int launch_sweep_spixl(hipStream_t s, int V, int W, int H, int S, const float* l
   long M = (long)mw * mh;
   int wps = (D + 63) / 64;
   wps = wps >= 3 ? 4 : wps;  // waves per superpixel: 1, 2 or 4
-  const int spb = 4 / wps;
+  const bool half = D <= 32;  // two superpixels per wave
+  const int spb = half ? 8 : 4 / wps;
   SweepArgs a{V, W, H, mw, mh, D, aw, z0, bl};
   const long nb = (M + spb - 1) / spb;
-  hipLaunchKernelGGL(k_sweep_spixl, dim3((unsigned)(8 * ((nb + 7) / 8)), (unsigned)(z1 - z0)), dim3(256), 0, s,
-                     (const float4*)lab, spixl, rep, levels, vs, sn, a, wps);
+  hipLaunchKernelGGL(half ? k_sweep_spixl<32> : k_sweep_spixl<64>, dim3((unsigned)(8 * ((nb + 7) / 8)),
+                     (unsigned)(z1 - z0)), dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a, wps);
   MVS_LAUNCH_CHECK("k_sweep_spixl");
   return 0;
 }

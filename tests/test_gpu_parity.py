@@ -105,6 +105,21 @@ def test_boundary_and_sweep(engine, name):
     assert_bits(sp.cpu().numpy()[..., 7], osp[..., 7], "s7")
 
 
+@pytest.mark.parametrize("dmax", [31, 32, 47, 100, 200])
+def test_sweep_level_counts(engine, dmax):
+    """k_sweep_spixl's lane layouts by level count: two superpixels per wave
+    (D <= 32), one wave (D <= 64), two or four waves per superpixel."""
+    c = dict(CASES["c3x1_s16"], dmin=0, dmax=dmax, seed=41)
+    b = build(c)
+    lab, sp, lb, rep = _chain(engine, c, b)
+    lab_h, sp_h, lb_h = lab.cpu().numpy(), sp.cpu().numpy(), as_u32(lb)
+    orep = orc.boundary(sp_h, lb_h, c["S"])
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
+    engine.sweep_spixl(lab, sp, rep, cam, c["S"])
+    osp = orc.sweep(lab_h, sp_h, orep, b["levels"], b["vs"], b["sn"], c["aw"], c["bl"], c["S"])
+    assert_bits(sp.cpu().numpy()[..., 7], osp[..., 7], f"s7 D={dmax + 1}")
+
+
 @pytest.mark.parametrize("name", list(PIXEL_CASES))
 def test_grid_and_pixel_sad(engine, name):
     c = PIXEL_CASES[name]

@@ -211,27 +211,33 @@ __device__ __forceinline__ float wave_tree(float v0, float v1, float v2, float v
   return s;
 }
 
+// One WAVE per superpixel (4 per workgroup): the wave walks the G window
+// tiles in order, each tile's 256 pixels as 4 per lane, tree-reduced in the
+// reference's order (wave_tree), and lane 0 sums the tile partials in tile
+// order -- no LDS, no barriers, and no idle waves when G < 4 (S = 8: G = 3,
+// the third tile entirely outside the 3S window).
 __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, const uint32_t* __restrict__ labels,
                                                 int W, int H, int S, int mw, int mh, int G, int cpl,
                                                 float* __restrict__ spixl) {
-  extern __shared__ float part[];  // [G][6]
-  int sp = blockIdx.x, z = blockIdx.y;
-  int gx = sp % mw, gy = sp / mw;
-  long P = (long)W * H;
+  const int lane = threadIdx.x & 63;
+  const int sp = blockIdx.x * 4 + (threadIdx.x >> 6), z = blockIdx.y;
+  if (sp >= mw * mh) return;  // whole wave; no barriers
+  const int gx = sp % mw, gy = sp / mw;
+  const long P = (long)W * H;
   const float4* L = lab + (long)z * P;
   const uint32_t* I = labels + (long)z * P;
-  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int lx = lane & 15, ly0 = lane >> 4;
-  for (int t = wave; t < G; t += 4) {
-    int nbx = t % cpl, nby = t / cpl;
+  const int lx = lane & 15, ly0 = lane >> 4;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < G; t++) {
+    const int nbx = t % cpl, nby = t / cpl;
     float v[4][6];
     bool any = false;
 #pragma unroll
     for (int m = 0; m < 4; m++) {
-      int ly = ly0 + 4 * m;
-      int pxo = nbx * kLocal + lx, pyo = nby * kLocal + ly;
-      int px = gx * S - S + pxo, py = gy * S - S + pyo;
-      bool in = pyo < S * 3 && pxo < S * 3 && py >= 0 && px >= 0 && px < W && py < H;
+      const int ly = ly0 + 4 * m;
+      const int pxo = nbx * kLocal + lx, pyo = nby * kLocal + ly;
+      const int px = gx * S - S + pxo, py = gy * S - S + pyo;
+      const bool in = pyo < S * 3 && pxo < S * 3 && py >= 0 && px >= 0 && px < W && py < H;
       bool mem = false;
       if (in) mem = I[(long)py * W + px] == (uint32_t)sp;
       float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -244,30 +250,17 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
       v[m][5] = mem ? 1.0f : 0.0f;
       any |= mem;
     }
-    float r[6];
+    float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (__any(any)) {
 #pragma unroll
       for (int c = 0; c < 6; c++) r[c] = wave_tree(v[0][c], v[1][c], v[2][c], v[3][c]);
-    } else {
-#pragma unroll
-      for (int c = 0; c < 6; c++) r[c] = 0.0f;
     }
-    if (lane == 0) {
 #pragma unroll
-      for (int c = 0; c < 6; c++) part[t * 6 + c] = r[c];
-    }
+    for (int c = 0; c < 6; c++) acc[c] = acc[c] + r[c];  // lane 0 holds the tile partial
   }
-  __syncthreads();
-  __shared__ float acc[6];
-  if (threadIdx.x < 6) {
-    float a = 0.0f;
-    for (int t = 0; t < G; t++) a = a + part[t * 6 + threadIdx.x];
-    acc[threadIdx.x] = a;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     float* o = spixl + 8 * ((long)z * mw * mh + sp);
-    float n = acc[5];
+    const float n = acc[5];
     o[0] = (float)sp;
     if (n != 0) {
       o[1] = acc[0] / n;
@@ -591,10 +584,8 @@ int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V
     MVS_LAUNCH_CHECK("k_update_finalize");
     return 0;
   }
-  size_t lds = sizeof(float) * 6 * (size_t)G;
-  if (lds > 64 * 1024) return arg_fail("spixl_size too large for the update kernel");
-  hipLaunchKernelGGL(k_update, dim3(mw * mh, V), dim3(256), lds, s, (const float4*)lab, labels, W, H, S, mw, mh, G,
-                     cpl, spixl);
+  hipLaunchKernelGGL(k_update, dim3((mw * mh + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, labels, W, H, S, mw,
+                     mh, G, cpl, spixl);
   MVS_LAUNCH_CHECK("k_update");
   return 0;
 }

@@ -253,3 +253,52 @@ def test_sweep_recovers_planar_disparity():
     gt = b["gt"][0] if b["gt"].ndim == 3 else b["gt"]
     inner = (slice(4, -4), slice(int(c["dmax"]) + 4, -4))
     assert np.mean(np.abs(d[inner] - gt[inner]) <= 1) > 0.6
+
+
+def _fused_wta_model(vol, levels, nw):
+    """numpy model of the fused sweep's winner-take-all (ncc.hip, FUSE): wave w
+    owns levels w, w+nw, ...; per pixel it folds (smallest cost, its level,
+    second smallest cost) in level order with strict <; the waves are merged
+    lexicographically for the best, and the smallest cost outside best +- 1 is
+    per wave its second smallest when its best level lies in the window, else
+    its smallest."""
+    D = vol.shape[0]
+    init = np.float32(1000000.0)
+    shp = vol.shape[1:]
+    v0 = np.full((nw,) + shp, init, np.float32)
+    v1 = np.full((nw,) + shp, init, np.float32)
+    i0 = np.full((nw,) + shp, -1, np.int64)
+    for dl in range(D):
+        w = dl % nw
+        c = vol[dl]
+        v1[w] = np.minimum(v1[w], np.maximum(v0[w], c))  # med3(v0, v1, c)
+        take = c < v0[w]
+        i0[w] = np.where(take, dl, i0[w])
+        v0[w] = np.minimum(v0[w], c)
+    bv, bi = v0[0].copy(), i0[0].copy()
+    for w in range(1, nw):
+        take = (v0[w] < bv) | ((v0[w] == bv) & (i0[w] >= 0) & (i0[w] < bi))
+        bv, bi = np.where(take, v0[w], bv), np.where(take, i0[w], bi)
+    c2 = np.full(shp, init, np.float32)
+    for w in range(nw):
+        inwin = (i0[w] >= bi - 1) & (i0[w] <= bi + 1)
+        c2 = np.minimum(c2, np.where(inwin, v1[w], v0[w]))
+    disp = np.where(bi >= 0, levels[np.maximum(bi, 0)], np.float32(0)).astype(np.float32)
+    conf = np.where((bi < 0) | (c2 == init), np.float32(0), c2 - bv).astype(np.float32)
+    return disp, conf
+
+
+@pytest.mark.parametrize("D", [1, 2, 3, 5, 9, 33, 128])
+@pytest.mark.parametrize("nw", [4, 8])
+def test_fused_wta_fold_equals_top4(D, nw):
+    """The fused kernel's per-wave fold + merge gives k_wta's top-4 answer
+    (oracle orc.wta), ties included: costs drawn from a few values so that
+    equal costs at many levels are common."""
+    rng = np.random.default_rng(1000 * D + nw)
+    vol = rng.choice(np.array([0.25, 0.5, 0.5, 1.0, 1.5, 2.0], np.float32), size=(D, 23, 37)).astype(np.float32)
+    vol[:, :3, :] = 2.0  # invalid-window rows: cost 2 at every level
+    levels = np.arange(D, dtype=np.float32) + np.float32(3)
+    od, oc = orc.wta(vol, levels)
+    fd, fc = _fused_wta_model(vol, levels, nw)
+    assert np.array_equal(fd.view(np.uint32), od.view(np.uint32))
+    assert np.array_equal(fc.view(np.uint32), oc.view(np.uint32))

@@ -5,20 +5,29 @@ stacks, 128 disparity hypotheses, NCC 5x5, SLIC K~2000 (BASELINE.json config 2).
 One step = the whole depth pipeline over one batch: for each of the V reference
 views of this rank's stack (inputs RGBx already resident in HBM): Lab
 conversion, SLIC (S=32, 5 update/assign iterations), superpixel extents, the
-reference superpixel SAD sweep, the per-pixel NCC 5x5 cost volume over 128
-hypotheses x 4 neighbours and its winner-take-all + confidence pass.
+reference superpixel SAD sweep, the per-pixel NCC 5x5 sweep over 128
+hypotheses x 4 neighbours and its winner-take-all + confidence.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--cost ncc|sad]
 
-N>1: launched by torch.distributed.run, one rank per GPU; every rank owns its
-own 5-view stack (independent objects, no data-path collective) -> weak scaling.
-Rank 0 prints ONE JSON line.
+`value` is the fused step (mvs_ncc_wta_d: the sweep kernel folds the WTA in,
+no cost volume in HBM).  The same invocation also times the two-pass step
+(materialised [D][H][W] volume + the k_wta streaming pass, bit-identical maps):
+`roofline` is k_wta's HBM read of that volume, the north star's roofline.
+
+N>1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the
+ranks come from the environment; `--gpus N` without WORLD_SIZE spawns the N
+rank processes itself before anything touches a GPU.  Every rank owns its own
+5-view stack (independent objects, no data-path collective) -> weak scaling;
+`view_sharded` adds C4 (one 32-view array sharded by reference view over the
+N GPUs, RCCL all-gathers) -> strong scaling.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -39,7 +48,7 @@ CONFIGS = {
     "c4": dict(aw=8, ah=4, W=1920, H=1080, S=32, dmin=0, dmax=127, K=5, nh=0, nv=0, knn=5, bl=1.0, cost="ncc",
                refine=True, filt=True, sharded=True,
                workload="32 reference views x 5 nearest neighbours, 1080p, one array sharded by reference view over "
-                        "the GPUs (RCCL all-gathers of labels/spixl, refinement state, disparity)"),
+                        "the GPUs (RCCL all-gathers of labels/spixl, refinement state, disparity, projections)"),
     # the reference's own defaults (clMVDE.cpp main): its algorithm exactly, no per-pixel sweep
     "ref": dict(aw=3, ah=3, W=1920, H=1080, S=8, dmin=30, dmax=60, K=5, nh=1, nv=1, bl=1.0359, cost="none",
                 refine=True,
@@ -48,14 +57,16 @@ CONFIGS = {
     "c5": dict(aw=5, ah=1, W=4096, H=3072, S=40, dmin=0, dmax=255, K=7, nh=4, nv=0, bl=1.0, cost="ncc",
                workload="5-view 4096x3072, 256 hypotheses, NCC 7x7, SLIC K=7931 (S=40)"),
 }
+METRIC = "Mpix/s depth (1080p, 128 depth hyp, 5 views) + depth L1 vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_PEAK = 1024 * 2.4e9 / 4.0  # wave64 VALU instructions/s: 1024 SIMDs x 2.4 GHz / 4 cycles
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -63,101 +74,245 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cost", default=None, choices=["ncc", "sad", "none"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the C4 view-sharded strong-scaling line")
+    ap.add_argument("--two-pass", action="store_true",
+                    help="headline = the two-pass step (cost volume in HBM + k_wta) instead of the fused sweep")
     ap.add_argument("--concurrent", action="store_true",
                     help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py)")
-    ap.add_argument("--fused", action="store_true",
-                    help="NCC sweep with the winner-take-all folded in (mvs_ncc_wta_d: no cost volume in HBM)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the launcher, rank setup, gathers and max-over-ranks timing on gloo")
+    return ap.parse_args(argv)
 
+
+# ---------------------------------------------------------------------------
+# launcher: one process per GPU
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_entry(rank, args, port):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    run(args)
+
+
+def main(argv=None):
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # spawn the ranks before anything initialises a GPU in this process
+        import torch.multiprocessing as mp
+        mp.start_processes(_rank_entry, args=(args, _free_port()), nprocs=args.gpus, join=True, start_method="spawn")
+        return
+    run(args)
+
+
+def _ranks():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def _max_over_ranks(x, device, world):
+    if world == 1:
+        return x
     import torch
     import torch.distributed as dist
+    t = torch.tensor([x], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed(step, steps, warmup, device, world, sync):
+    """W untimed warmup steps, then EXACTLY K steps between barrier + sync on
+    both sides; the max over ranks of the elapsed time, and the last output."""
+    import torch.distributed as dist
+    out = None
+    for _ in range(warmup):
+        out = step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    sync()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    return _max_over_ranks(t1 - t0, device, world), out
+
+
+def run(args):
+    world, rank, local = _ranks()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world
+    try:
+        res = bench(args, world, rank, local)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def dry_run(args, world, rank):
+    """The launch/timing/reporting path without a GPU: gloo ranks, one
+    ViewGather (the product's all-gather) of a 5-view block per step."""
+    import torch
+    import torch.distributed as dist
+
+    from cl_multiview_stereo_amd.distributed import ViewGather
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world
+    g = ViewGather(5 * world)
+    full = torch.zeros((5 * world, 64, 64))
+    z0, z1 = g.block
+
+    def step():
+        full[z0:z1] = float(rank + 1)
+        return g(full[z0:z1], full)
+
+    el, out = timed(step, args.steps, args.warmup, "cpu", world, lambda: None)
+    ok = all(bool((out[b0:b1] == r + 1).all()) for r, (b0, b1) in enumerate(g.blocks))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(el * 1e3 / max(args.steps, 1), 4),
+                          "dry_run": True, "gather_ok": ok, "world_size": world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def _pmc_traffic(name, W, H, D):
+    """Corrected HBM bytes per launch of k_wta from this configuration's own
+    PMC pass (profiles/pmc_wta_<config>.json, written by scripts/pmc_wta.sh),
+    or None when no pass of this exact shape exists."""
+    p = os.path.join(ROOT, "profiles", f"pmc_wta_{name}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        j = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    if (j.get("W"), j.get("H"), j.get("D")) != (W, H, D):
+        return None
+    return j.get("hbm_bytes_per_launch")
+
+
+def _valu_insts(name, cost, fused):
+    """SQ_INSTS_VALU per launch of the NCC sweep (profiles/pmc_ncc.json, C2),
+    launch-weighted over the band-width variants."""
+    pmc_ncc = os.path.join(ROOT, "profiles", "pmc_ncc.json")
+    if name != "c2" or cost != "ncc" or not os.path.exists(pmc_ncc):
+        return None
+    tag = "true>" if fused else "false>"
+    ent = [v for k, v in json.load(open(pmc_ncc)).items() if k.startswith("k_ncc_volume") and k.endswith(tag)]
+    if not ent:
+        return None
+    wts = [e.get("launches", 1) for e in ent]
+    return sum(e["valu_wave_insts_per_launch"] * w for e, w in zip(ent, wts)) / sum(wts)
+
+
+def bench(args, world, rank, local):
+    import torch
 
     from cl_multiview_stereo_amd import params, synth
     from cl_multiview_stereo_amd.engine import Engine
     from cl_multiview_stereo_amd.pipeline import Pipeline
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = dict(CONFIGS[args.config])
     cost = args.cost or cfg["cost"]
     V = cfg["aw"] * cfg["ah"]
     W, H = cfg["W"], cfg["H"]
+    D = cfg["dmax"] - cfg["dmin"] + 1
     st = params.Settings(spixl_size=cfg["S"], array_width=cfg["aw"], array_height=cfg["ah"], min_disp=cfg["dmin"],
                          max_disp=cfg["dmax"], inc=1, neib_hor=cfg["nh"], neib_ver=cfg["nv"], bl_ratio=cfg["bl"],
                          window=cfg["K"], cost=cost)
-    D = cfg["dmax"] - cfg["dmin"] + 1
-
     e = Engine(local)
+    dev = e.device
+    sync = torch.cuda.synchronize
     sharded = bool(cfg.get("sharded"))
+    fused = cost == "ncc" and not args.two_pass
     # independent stacks per rank (weak scaling) or one array sharded by view (strong)
     stack, _ = synth.make_stack(W, H, cfg["aw"], cfg["ah"], cfg["dmin"], cfg["dmax"], cfg["bl"],
                                 0x5EED + 2 + (0 if sharded else rank))
-    rgbx = torch.from_numpy(stack).to(e.device)
-    vlists = (params.nearest_neighbours(cfg["aw"], cfg["ah"], cfg["knn"]) if cfg.get("knn") else None)
-    pipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,
-                    refine=bool(cfg.get("refine")),
-                    filt=bool(cfg.get("filt")) and not sharded, concurrent=args.concurrent, fused=args.fused)
-    if sharded:
-        from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
-        spipe = ShardedPipeline(EngineBackend(e, fused=args.fused), st, pipe.cam, ViewGather(V), pixel_cost=cost, refine=True,
-                                filt=bool(cfg.get("filt")))
+    rgbx = torch.from_numpy(stack).to(dev)
+    vlists = params.nearest_neighbours(cfg["aw"], cfg["ah"], cfg["knn"]) if cfg.get("knn") else None
 
-    # HIP events around the cost-volume kernels, on the stream they run on
+    # HIP events around the sweep / WTA launches, on the stream they run on
     timers = {"wta": [], "ncc": [], "fused": []}
-    if pipe.pixel is not None and cost == "ncc":
-        orig_wta, orig_vol = e.wta, e.ncc_volume
+    recording = [False]
 
-        def timed(name, fn):
-            def w(*a, **k):
-                s = torch.cuda.Event(enable_timing=True)
-                t = torch.cuda.Event(enable_timing=True)
-                s.record()
-                r = fn(*a, **k)
-                t.record()
-                if timing[0]:
-                    timers[name].append((s, t))
-                return r
-            return w
-        timing = [False]
-        e.wta = timed("wta", orig_wta)
-        e.ncc_volume = timed("ncc", orig_vol)
-        e.ncc_wta = timed("fused", e.ncc_wta)
-    else:
-        timing = [False]
+    def instrument(name, fn):
+        def w(*a, **k):
+            s = torch.cuda.Event(enable_timing=True)
+            t = torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = fn(*a, **k)
+            t.record()
+            if recording[0]:
+                timers[name].append((s, t))
+            return r
+        return w
 
-    def step():
-        return spipe.run(rgbx) if sharded else pipe.exe_pipeline(rgbx)
+    e.wta = instrument("wta", e.wta)
+    e.ncc_volume = instrument("ncc", e.ncc_volume)
+    e.ncc_wta = instrument("fused", e.ncc_wta)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timing[0] = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    timing[0] = False
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=e.device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    def avg(lst):
+        return sum(s.elapsed_time(t) for s, t in lst) / len(lst) * 1e-3
+
+    def make(fz):
+        p = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,
+                     refine=bool(cfg.get("refine")), filt=bool(cfg.get("filt")) and not sharded,
+                     concurrent=args.concurrent, fused=fz)
+        if not sharded:
+            return p, (lambda: p.exe_pipeline(rgbx))
+        from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
+        sp = ShardedPipeline(EngineBackend(e, fused=fz), st, p.cam, ViewGather(V), pixel_cost=cost, refine=True,
+                             filt=bool(cfg.get("filt")))
+        return p, (lambda: sp.run(rgbx))
+
+    pipe, step = make(fused)
+    recording[0] = True
+    elapsed, out = timed(step, args.steps, args.warmup, dev, world, sync)
+    recording[0] = False
     ms_per_step = elapsed * 1e3 / max(args.steps, 1)
     units = V if sharded else world * V  # reference views processed per step, whole job
     mpix = units * W * H * args.steps / elapsed / 1e6
+    head_timers = {k: list(v) for k, v in timers.items()}
 
     res = {
-        "metric": "Mpix/s depth (1080p, 128 depth hyp, 5 views) + depth L1 vs ref",
+        "metric": METRIC,
         "value": round(mpix, 3),
         "unit": "Mpix/s",
         "n_gpus": world,
@@ -167,131 +322,142 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
-        "dtype": "f32/i32",
+        "dtype": ("i8 (NCC: 8-bit intensities as int8 v_dot4 operands, i32 window sums, f32 costs; "
+                  "SLIC / superpixel SAD / refinement in f32 with the reference's f64 promotions)") if cost == "ncc"
+                 else "f32 (Lab SAD, the reference's arithmetic; f64 where its double literals promote)",
         "data": "synthetic (seeded rendered camera-array stack, RGBx resident in HBM)",
         "config": {"workload": cfg["workload"], "views": V, "width": W, "height": H, "hypotheses": D,
                    "window": cfg["K"], "cost": cost, "spixl_size": cfg["S"],
                    "neighbours": int(pipe.cam.subset_num.max()),
+                   "sweep": ("fused sweep + WTA (no cost volume in HBM)" if fused else
+                             "two-pass (cost volume in HBM + k_wta)") if cost == "ncc" else cost,
                    "parallelism": (f"views sharded over {world} GPU(s)" if sharded else
                                    f"view-stack per GPU x{world}"),
                    "refinement": bool(cfg.get("refine")), "consistency_filter": bool(cfg.get("filt"))},
     }
-
-    def avg(lst):
-        return sum(s.elapsed_time(t) for s, t in lst) / len(lst) * 1e-3
-
-    def valu_insts(fused):
-        # SQ_INSTS_VALU per launch (profiles/pmc_ncc.json, C2), launch-weighted over
-        # the band-width variants of the plain (FUSE=false) or fused kernel
-        pmc_ncc = os.path.join(ROOT, "profiles", "pmc_ncc.json")
-        if args.config != "c2" or cost != "ncc" or not os.path.exists(pmc_ncc):
-            return None
-        tag = "true>" if fused else "false>"
-        ent = [v for k, v in json.load(open(pmc_ncc)).items() if k.startswith("k_ncc_volume") and k.endswith(tag)]
-        if not ent:
-            return None
-        wts = [e.get("launches", 1) for e in ent]
-        return sum(e["valu_wave_insts_per_launch"] * w for e, w in zip(ent, wts)) / sum(wts)
-
-    VALU_PEAK = 1024 * 2.4e9 / 4.0  # wave64 VALU ops/s: 1024 SIMDs x 2.4 GHz / 4 cycles
-    if args.fused and timers["fused"]:
-        # no volume: the fused sweep is VALU-issue-bound
-        t_ncc = avg(timers["fused"])
-        insts = valu_insts(True)
-        res["roofline"] = {"bound": "valu", "kernel": "k_ncc_volume<..., FUSE=true> (sweep + WTA, no volume)",
-                           "achieved": None if insts is None else round(insts / t_ncc / 1e9, 1),
-                           "peak": VALU_PEAK / 1e9, "unit": "G wave-instructions/s",
-                           "frac": None if insts is None else round(insts / t_ncc / VALU_PEAK, 4),
-                           "traffic": None, "avg_launch_ms": round(t_ncc * 1e3, 4)}
-    if timers["wta"]:
-        t_wta = avg(timers["wta"])
-        t_ncc = avg(timers["ncc"])
-        wta_bytes = 4.0 * D * W * H + 8.0 * W * H  # volume read + disparity/confidence write
-        achieved = wta_bytes / t_wta / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_wta.json")
-        if os.path.exists(pmc):
-            try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        res["roofline"] = {"bound": "hbm", "kernel": "k_wta (cost-volume read pass)", "achieved": round(achieved, 1),
-                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                           "traffic": traffic, "algorithmic_bytes_per_launch": wta_bytes,
-                           "avg_launch_ms": round(t_wta * 1e3, 4)}
+    if fused and head_timers["fused"]:
+        t_f = avg(head_timers["fused"])
         cells = float(D) * W * H
         nbr = max(1, int(pipe.cam.subset_num[0]))
-        vol_bytes = 4.0 * cells
-        res["roofline_sweep"] = {"kernel": "k_ncc_volume (cost-volume write pass)", "avg_launch_ms": round(t_ncc * 1e3, 4),
-                                 "view_cells_per_s": round(cells * nbr / t_ncc / 1e9, 3),
-                                 "unit_view_cells": "G view-cells/s",
-                                 "hbm_write_GBps": round(vol_bytes / t_ncc / 1e9, 1),
-                                 "hbm_write_frac": round(vol_bytes / t_ncc / 1e9 / HBM_PEAK_GBS, 4)}
-        # VALU issue bound of the producer (its binding resource): wave-instructions per
-        # launch from the SQ_INSTS_VALU pass (profiles/pmc_ncc.json, C2) at one
-        # instruction per 4 cycles per SIMD, 1024 SIMDs, 2.4 GHz
-        insts = valu_insts(False)
+        insts = _valu_insts(args.config, cost, True)
+        res["roofline_sweep"] = {
+            "kernel": "k_ncc_volume<..., FUSE=true> (sweep + WTA, the headline step's dominant kernel)",
+            "bound": "valu", "avg_launch_ms": round(t_f * 1e3, 4),
+            "view_cells_per_s": round(cells * nbr / t_f / 1e9, 3), "unit_view_cells": "G view-cells/s"}
         if insts is not None:
-            res["roofline_sweep"].update({"bound": "valu", "valu_wave_insts_per_launch": round(insts),
-                                          "valu_issue_frac": round(insts / t_ncc / VALU_PEAK, 4),
+            res["roofline_sweep"].update({"valu_wave_insts_per_launch": round(insts),
+                                          "valu_issue_frac": round(insts / t_f / VALU_PEAK, 4),
                                           "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op"})
 
-    # the same step with the WTA folded into the sweep kernel (no cost volume in
-    # HBM): timed with the same protocol after the headline run, outputs
-    # compared bit-for-bit with the headline step's
-    if cost == "ncc" and not args.fused and not sharded and not cfg.get("refine"):
-        fpipe = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=cost, fused=True)
-        for _ in range(max(1, args.warmup)):
-            fout = fpipe.exe_pipeline(rgbx)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        timing[0] = True
-        f0 = time.perf_counter()
-        for _ in range(args.steps):
-            fout = fpipe.exe_pipeline(rgbx)
-        torch.cuda.synchronize()
-        fel = time.perf_counter() - f0
-        timing[0] = False
-        if world > 1:
-            dist.barrier()
-            tt = torch.tensor([fel], device=e.device, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            fel = float(tt.item())
-        same = bool(torch.equal(fout.disp.view(torch.int32), out.disp.view(torch.int32)) and
-                    torch.equal(fout.conf.view(torch.int32), out.conf.view(torch.int32)))
-        res["fused_variant"] = {"what": "bench.py --fused: k_ncc_volume with the WTA folded in, no cost volume in HBM",
-                                "value": round(units * W * H * args.steps / fel / 1e6, 3), "unit": "Mpix/s",
-                                "ms_per_step": round(fel * 1e3 / max(args.steps, 1), 4),
-                                "bit_identical_to_headline": same,
-                                "sweep_avg_launch_ms": round(avg(timers["fused"]) * 1e3, 4) if timers["fused"] else None}
-        fi = valu_insts(True)
-        if fi is not None and timers["fused"]:
-            res["fused_variant"]["valu_issue_frac"] = round(fi / avg(timers["fused"]) / VALU_PEAK, 4)
+    # the two-pass step (cost volume in HBM + k_wta), same protocol: the
+    # north star's roofline is k_wta's read of that volume
+    if cost == "ncc":
+        tp_out = out
+        if fused:
+            _, tp_step = make(False)
+            for k in timers:
+                timers[k].clear()
+            recording[0] = True
+            tp_el, tp_out = timed(tp_step, args.steps, max(1, args.warmup), dev, world, sync)
+            recording[0] = False
+            same = all(torch.equal(getattr(tp_out, f).view(torch.int32), getattr(out, f).view(torch.int32))
+                       for f in ("disp", "conf") if getattr(out, f, None) is not None)
+            res["two_pass_variant"] = {"what": "the same step with the cost volume materialised in HBM + k_wta",
+                                       "value": round(units * W * H * args.steps / tp_el / 1e6, 3), "unit": "Mpix/s",
+                                       "ms_per_step": round(tp_el * 1e3 / max(args.steps, 1), 4),
+                                       "bit_identical_to_headline": bool(same)}
+        if timers["wta"]:
+            t_wta = avg(timers["wta"])
+            t_ncc = avg(timers["ncc"])
+            wta_bytes = 4.0 * D * W * H + 8.0 * W * H  # volume read + disparity/confidence write
+            achieved = wta_bytes / t_wta / 1e9
+            res["roofline"] = {"bound": "hbm",
+                               "kernel": "k_wta (cost-volume read pass of the two-pass step, timed in this run)",
+                               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(achieved / HBM_PEAK_GBS, 4),
+                               "traffic": _pmc_traffic(args.config, W, H, D),
+                               "algorithmic_bytes_per_launch": wta_bytes, "avg_launch_ms": round(t_wta * 1e3, 4)}
+            cells = float(D) * W * H
+            nbr = max(1, int(pipe.cam.subset_num[0]))
+            sw = {"kernel": "k_ncc_volume (cost-volume write pass)", "avg_launch_ms": round(t_ncc * 1e3, 4),
+                  "view_cells_per_s": round(cells * nbr / t_ncc / 1e9, 3), "unit_view_cells": "G view-cells/s",
+                  "hbm_write_GBps": round(4.0 * cells / t_ncc / 1e9, 1),
+                  "hbm_write_frac": round(4.0 * cells / t_ncc / 1e9 / HBM_PEAK_GBS, 4)}
+            insts = _valu_insts(args.config, cost, False)
+            if insts is not None:
+                sw.update({"bound": "valu", "valu_wave_insts_per_launch": round(insts),
+                           "valu_issue_frac": round(insts / t_ncc / VALU_PEAK, 4)})
+            res.setdefault("two_pass_variant", {})["roofline_sweep"] = sw
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and (not cfg.get("refine") or cost == "none"):
+    # PCIe-inclusive rate: the RGBx stack H2D from pinned host memory and the
+    # disparity maps D2H inside the timed region (never `value`)
+    if not sharded and world == 1 and hasattr(out, "disp"):
+        host_in = torch.from_numpy(stack).pin_memory()
+        src = out.disp_refined if out.disp is None else out.disp
+        host_out = torch.empty(tuple(src.shape), dtype=torch.float32).pin_memory()
+        dev_in = torch.empty_like(rgbx)
+
+        def pstep():
+            dev_in.copy_(host_in, non_blocking=True)
+            o = pipe.exe_pipeline(dev_in)  # the headline pipeline
+            host_out.copy_(o.disp_refined if o.disp is None else o.disp, non_blocking=True)
+            return o
+
+        p_el, _ = timed(pstep, args.steps, 1, dev, world, sync)
+        res["pcie_inclusive"] = {"value": round(V * W * H * args.steps / p_el / 1e6, 3), "unit": "Mpix/s",
+                                 "ms_per_step": round(p_el * 1e3 / max(args.steps, 1), 4),
+                                 "what": f"H2D of the {stack.nbytes / 1e6:.1f} MB RGBx stack (pinned) + the step "
+                                         f"+ D2H of the {host_out.numel() * 4 / 1e6:.1f} MB disparity maps"}
+
+    # C4: one 32-view array sharded by reference view over the N GPUs (strong scaling)
+    if not args.no_sharded and args.config in ("c2",) and cost == "ncc":
+        res["view_sharded"] = view_sharded(args, e, world, rank, sync)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not sharded:
         try:
-            res["cpu_baseline"], res["depth_l1_vs_oracle"] = cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out)
+            res["cpu_baseline"], res["depth_l1_vs_oracle"] = cpu_baseline(pipe, stack, cfg, cost, out)
         except Exception as ex:  # report, never hide
             res["cpu_baseline"] = {"error": repr(ex)}
-    if rank == 0:
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    return res
 
 
-def cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out):
+def view_sharded(args, e, world, rank, sync):
+    """C4 at this world size: 32 reference views x 5 nearest neighbours, 1080p,
+    each rank owning a contiguous block of views (distributed.py)."""
+    import torch
+
+    from cl_multiview_stereo_amd import params, synth
+    from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
+    from cl_multiview_stereo_amd.engine import CameraArray
+    c = CONFIGS["c4"]
+    V, W, H = c["aw"] * c["ah"], c["W"], c["H"]
+    st = params.Settings(spixl_size=c["S"], array_width=c["aw"], array_height=c["ah"], min_disp=c["dmin"],
+                         max_disp=c["dmax"], inc=1, bl_ratio=c["bl"], window=c["K"], cost="ncc")
+    stack, _ = synth.make_stack(W, H, c["aw"], c["ah"], c["dmin"], c["dmax"], c["bl"], 0x5EED + 4)
+    rgbx = torch.from_numpy(stack).to(e.device)
+    mat, num = params.flatten_subsets(params.nearest_neighbours(c["aw"], c["ah"], c["knn"]))
+    cam = CameraArray(c["aw"], c["bl"], params.disparity_levels(c["dmin"], c["dmax"], 1), mat, num)
+    g = ViewGather(V)
+    sp = ShardedPipeline(EngineBackend(e, fused=True), st, cam, g, pixel_cost="ncc", refine=True, filt=True)
+    steps = max(3, args.steps // 2)
+    el, _ = timed(lambda: sp.run(rgbx), steps, max(1, args.warmup), e.device, world, sync)
+    return {"workload": c["workload"], "value": round(V * W * H * steps / el / 1e6, 3), "unit": "Mpix/s",
+            "ms_per_step": round(el * 1e3 / steps, 4), "steps": steps, "n_gpus": world, "scaling": "strong",
+            "views_per_gpu": g.block[1] - g.block[0], "sweep": "fused NCC sweep + WTA"}
+
+
+def cpu_baseline(pipe, stack, cfg, cost, out):
     """The oracle (CPU restatement, OpenMP) runs ONE full step of the same
     workload on this host: cvt + SLIC of every view, extents, the superpixel
-    sweep and the per-pixel sweep + WTA of every reference view.  At C2 that
-    is ~10 s on 16 threads.  Returns (cpu_baseline, depth L1 of the timed GPU
-    step's disparity maps against the oracle's, over all reference views)."""
+    sweep, the per-pixel sweep + WTA of every reference view, and (C3 / ref)
+    the refinement + fusion and the consistency filter.  At C2 that is ~10 s
+    on 16 threads.  Returns (cpu_baseline, depth L1 of the timed GPU step's
+    maps against the oracle's)."""
     import torch
 
     from oracle import oracle as orc
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     os.environ["OMP_NUM_THREADS"] = str(threads)
     W, H, S = cfg["W"], cfg["H"], cfg["S"]
     cam = pipe.cam
@@ -304,24 +470,35 @@ def cpu_baseline(e, pipe, stack, cfg, cost, rgbx, out):
     rep = orc.boundary(sp, lb, S)
     sp = orc.sweep(lab_all, sp, rep, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"], S)
     t_seg = time.perf_counter() - t0
-    if cost == "none":  # the reference pipeline: refinement + fusion of every view
-        od = orc.refine(sp, lb, rep, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"], S)["disp"]
-    elif cost == "ncc":
+    maps = {}
+    if cost == "ncc":
         q = orc.l8(lab_all)
-        od = np.stack([orc.wta(orc.ncc_volume(q, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"],
-                                              cfg["K"], z), cam.levels)[0] for z in range(V)])
-    else:
-        od = orc.sweep_pixel_sad(lab_all, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"])
+        maps["disp"] = np.stack([orc.wta(orc.ncc_volume(q, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"],
+                                                        cfg["bl"], cfg["K"], z), cam.levels)[0] for z in range(V)])
+    elif cost == "sad":
+        maps["disp"] = orc.sweep_pixel_sad(lab_all, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"])
+    if cfg.get("refine"):
+        maps["disp_refined"] = orc.refine(sp, lb, rep, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"],
+                                          S)["disp"]
+        if cfg.get("filt"):
+            maps["disp_filtered"] = orc.filt(maps["disp_refined"], cfg["aw"], cfg["bl"], 1.0)[1]
     t_all = time.perf_counter() - t0
     cpu = {"value": round(V * W * H / t_all / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
-           "sample": f"one full step of the bench workload ({V} reference views, {len(cam.levels)} hypotheses) on "
-                     f"oracle/mvs_oracle.c, OpenMP x{threads}: {t_all:.1f}s (segmentation+superpixel sweep "
-                     f"{t_seg:.1f}s)"}
+           "sample": f"one full step of the bench workload ({V} reference views, {len(cam.levels)} hypotheses"
+                     f"{', refinement' if cfg.get('refine') else ''}{', filter' if cfg.get('filt') else ''}) on "
+                     f"oracle/mvs_oracle.c, OpenMP x{threads}: {t_all:.1f}s (segmentation + superpixel sweep "
+                     f"{t_seg:.1f}s)",
+           **_cpu_info()}
     torch.cuda.synchronize()
-    gd = (out.disp_refined if cost == "none" else out.disp).cpu().numpy()
-    l1 = float(np.abs(gd - od).mean())
-    return cpu, {"value": l1, "unit": "px (mean |d_gpu - d_oracle|)", "bit_exact": bool(np.array_equal(gd, od)),
-                 "sample": f"the last timed step's disparity maps, all {V} reference views, {W}x{H}"}
+    l1 = {}
+    for k, od in maps.items():
+        gd = getattr(out, k).cpu().numpy()
+        l1[k] = {"value": float(np.abs(gd - od).mean()), "bit_exact": bool(np.array_equal(gd, od))}
+    head = "disp" if "disp" in l1 else ("disp_filtered" if "disp_filtered" in l1 else "disp_refined")
+    res = {"value": l1[head]["value"], "unit": "px (mean |d_gpu - d_oracle|)", "bit_exact": l1[head]["bit_exact"],
+           "map": head, "maps": l1,
+           "sample": f"the last timed step's disparity maps, all {V} reference views, {W}x{H}"}
+    return cpu, res
 
 
 if __name__ == "__main__":

@@ -280,7 +280,32 @@ int mvs_sweep_pixel_sad_d(mvs_ctx* c, int W, int H, const float* lab, const mvs_
 int mvs_box_stats_d(mvs_ctx* c, const uint8_t* l8, int V, int W, int H, int K, int32_t* box) {
   if (!c || !l8 || !box || V <= 0 || bad_dims(W, H) || (K != 5 && K != 7))
     return mvs::arg_fail("mvs_box_stats_d: bad arguments (K must be 5 or 7)");
-  return mvs::launch_box_stats(c->stream, l8, V, W, H, K, box);
+  return mvs::launch_box_stats(c->stream, l8, V, W, H, K, box, 0, V);
+}
+
+int mvs_box_stats_range_d(mvs_ctx* c, const uint8_t* l8, int V, int W, int H, int K, int z0, int z1, int32_t* box) {
+  if (!c || !l8 || !box || V <= 0 || bad_dims(W, H) || (K != 5 && K != 7) || z0 < 0 || z1 > V || z0 > z1)
+    return mvs::arg_fail("mvs_box_stats_range_d: bad arguments (K must be 5 or 7, 0 <= z0 <= z1 <= V)");
+  return mvs::launch_box_stats(c->stream, l8, V, W, H, K, box, z0, z1);
+}
+
+int mvs_set_ncc_variant(mvs_ctx* c, int waves, int levels_per_wave, int band_w, int general_rows) {
+  if (!c) return mvs::arg_fail("null context");
+  if ((waves != 0 && waves != 4 && waves != 8) || (levels_per_wave != 0 && levels_per_wave != 1 &&
+      levels_per_wave != 2 && levels_per_wave != 4) || (band_w != 0 && band_w != 128 && band_w != 192 &&
+      band_w != 256) || (waves == 8 && levels_per_wave != 0 && levels_per_wave != 4))
+    return mvs::arg_fail("mvs_set_ncc_variant: waves 0|4|8, levels_per_wave 0|1|2|4 (8 waves: 4), band_w 0|128|192|256");
+  c->ncc_nw = waves;
+  c->ncc_dpw = levels_per_wave;
+  c->ncc_bw = band_w;
+  c->ncc_general = general_rows ? 1 : 0;
+  return 0;
+}
+
+int mvs_ncc_last_variant(mvs_ctx* c, int32_t* out7) {
+  if (!c || !out7) return mvs::arg_fail("mvs_ncc_last_variant: null argument");
+  for (int i = 0; i < 7; i++) out7[i] = c->ncc_last[i];
+  return 0;
 }
 
 int mvs_ncc_volume_d(mvs_ctx* c, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a, int K,
@@ -318,7 +343,19 @@ int mvs_init_state_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const 
     return mvs::arg_fail("mvs_init_state_d: bad arguments");
   RC(upload_meta(c, a));
   return mvs::launch_init_state(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, rep,
-                                flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state);
+                                flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state, 0,
+                                a->view_count);
+}
+
+int mvs_init_state_range_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                           const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
+                           int kernel_steps, float kss, float fuse, int z0, int z1, float* state) {
+  if (!c || !spixl || !labels || !rep || !flat || !state || S <= 0 || bad_dims(W, H))
+    return mvs::arg_fail("mvs_init_state_range_d: bad arguments");
+  RC(upload_meta(c, a));
+  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_init_state_range_d: bad view range");
+  return mvs::launch_init_state(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, rep,
+                                flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state, z0, z1);
 }
 
 int mvs_propagate_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels, const uint8_t* rep,
@@ -383,6 +420,22 @@ int mvs_filter_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_rati
     return mvs::arg_fail("mvs_filter_d: bad arguments");
   return mvs::launch_filter(c->stream, V, W, H, array_width, bl_ratio, (float)(0.5 * (double)fuse), disp_full, proj,
                             out, z0, z1);
+}
+
+int mvs_proj_inv_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, const float* disp_full,
+                   float* proj, int z0, int z1) {
+  if (!c || !disp_full || !proj || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V || z0 > z1)
+    return mvs::arg_fail("mvs_proj_inv_d: bad arguments");
+  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1);
+}
+
+int mvs_remove_inconsistency_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, float fuse,
+                               const float* disp_full, const float* proj, float* out, int z0, int z1) {
+  if (!c || !disp_full || !proj || !out || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V ||
+      z0 > z1)
+    return mvs::arg_fail("mvs_remove_inconsistency_d: bad arguments");
+  return mvs::launch_remove_incons(c->stream, V, W, H, array_width, bl_ratio, (float)(0.5 * (double)fuse), disp_full,
+                                   proj, out, z0, z1);
 }
 
 // ---- host-pointer API (reference stage methods) ----------------------------------

@@ -29,6 +29,10 @@ struct mvs_ctx {
   // small host-built launch plans (e.g. the NCC shift tables), uploaded once
   // per distinct content and kept for the life of the context
   std::map<std::vector<int32_t>, int32_t*> plans;
+  // NCC sweep variant override (mvs_set_ncc_variant; 0 = automatic) and the
+  // variant of the last launch {K, TH, DPW, NW, BW, EVEN, FUSE}
+  int ncc_nw = 0, ncc_dpw = 0, ncc_bw = 0, ncc_general = 0;
+  int ncc_last[7] = {0, 0, 0, 0, 0, 0, 0};
 };
 
 namespace mvs {
@@ -80,7 +84,7 @@ int launch_sweep_spixl(hipStream_t s, int V, int W, int H, int S, const float* l
 int launch_sweep_pixel_sad(hipStream_t s, int V, int W, int H, const float* lab, const float* levels, int D,
                            const int* vs, const int* sn, const int* sn_host, int aw, float bl, int z0, int z1,
                            float* disp);
-int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box);
+int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box, int z0, int z1);
 int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
                       const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol,
                       const float* levels_dev = nullptr, float* disp = nullptr, float* conf = nullptr);
@@ -90,7 +94,8 @@ int launch_wta(hipStream_t s, int W, int H, int D, const float* vol, const float
 int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat);
 int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
                       const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
-                      const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state);
+                      const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state,
+                      int z0, int z1);
 int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
                      const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
                      const int* sn, int iter, float alpha, float gamma, float fuse, int nks, float kss,
@@ -99,5 +104,9 @@ int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float
                           const uint32_t* labels, const float* state, float* disp);
 int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
                   float* proj, float* out, int z0, int z1);
+int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const float* full, float* proj, int z0,
+                    int z1);
+int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
+                         const float* proj, float* out, int z0, int z1);
 
 }  // namespace mvs

@@ -61,11 +61,11 @@ __host__ __device__ __forceinline__ long pair_index(int y, int x, int W) {
 constexpr int BS_TW = 64, BS_TH = 16;
 template <int R>
 __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q, int W, int H,
-                                                   uint2* __restrict__ stats, uint2* __restrict__ pk) {
+                                                   int z0, uint2* __restrict__ stats, uint2* __restrict__ pk) {
   constexpr int K = 2 * R + 1, NK = K * K;
   constexpr int TW = BS_TW + 8, TR = BS_TH + 2 * R;  // tile covers columns x0-R .. x0+63-R+7
   __shared__ uint8_t t[TR][TW + 4];
-  const int x0 = blockIdx.x * BS_TW, y0 = blockIdx.y * BS_TH, z = blockIdx.z;
+  const int x0 = blockIdx.x * BS_TW, y0 = blockIdx.y * BS_TH, z = z0 + blockIdx.z;
   const int Hp = H + (H & 1);
   const long Pv = (long)W * Hp;  // plane elements per view
   const uint8_t* Q = q + z * (long)W * H;
@@ -552,8 +552,11 @@ NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const fl
 }
 
 template <int K, int TH, int DPW, int NW, int BW, bool EVEN>
-int launch_ncc_bw(hipStream_t s, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
+int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
                   const WtaOut& wo, size_t lds) {
+  hipStream_t s = ctx->stream;
+  const int variant[7] = {K, TH, DPW, NW, BW, EVEN ? 1 : 0, vol ? 0 : 1};
+  std::copy(variant, variant + 7, ctx->ncc_last);
   constexpr int DC = NW * DPW;
   a.tiles_x = (a.W + 63) / 64;
   a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);
@@ -575,35 +578,41 @@ template <int K, int TH, int DPW, int NW>
 int launch_ncc_t(mvs_ctx* ctx, const uint2* stats, const uint2* pk, NccArgs& a, const float* levels_host,
                  const float* fdx, const float* fdy, float bl, float* vol, const WtaOut& wo, size_t lds_cap) {
   NccPlan p = make_plan<K, TH, DPW, NW>(levels_host, a.D, a.nn, fdx, fdy, bl);
-  const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * p.band_w;
-  if (lds > lds_cap || p.band_w > 256) return 1;
+  // the band's pair-row stride is the template BW: the smallest of 128 / 192 /
+  // 256 holding band_w, or a wider one forced through mvs_set_ncc_variant
+  const int bw = std::max(std::max(p.band_w, ctx->ncc_bw), 128);
+  const int bwt = bw <= 128 ? 128 : bw <= 192 ? 192 : 256;
+  const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * bwt;
+  if (lds > lds_cap || bw > 256) return 1;
   int rc = 0;
   const int32_t* dev = plan_upload(ctx, p.table, &rc);
   if (rc) return rc;
   a.pk_pairs = p.pk_pairs;
   a.st_pairs = p.st_pairs;
   const NccRec* plan = (const NccRec*)dev;
-  if (p.even) {
-    if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, NW, 128, true>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
-    if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, NW, 192, true>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
-    return launch_ncc_bw<K, TH, DPW, NW, 256, true>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
+  if (p.even && !ctx->ncc_general) {
+    if (bwt == 128) return launch_ncc_bw<K, TH, DPW, NW, 128, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+    if (bwt == 192) return launch_ncc_bw<K, TH, DPW, NW, 192, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+    return launch_ncc_bw<K, TH, DPW, NW, 256, true>(ctx, stats, pk, plan, a, vol, wo, lds);
   }
-  if (p.band_w <= 128) return launch_ncc_bw<K, TH, DPW, NW, 128, false>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
-  if (p.band_w <= 192) return launch_ncc_bw<K, TH, DPW, NW, 192, false>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
-  return launch_ncc_bw<K, TH, DPW, NW, 256, false>(ctx->stream, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 128) return launch_ncc_bw<K, TH, DPW, NW, 128, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 192) return launch_ncc_bw<K, TH, DPW, NW, 192, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+  return launch_ncc_bw<K, TH, DPW, NW, 256, false>(ctx, stats, pk, plan, a, vol, wo, lds);
 }
 
 }  // namespace
 
-int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box) {
+// window planes of views [z0, z1) of a V-view box buffer
+int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box, int z0, int z1) {
+  if (z1 <= z0) return 0;
   const int Hp = H + (H & 1);
   uint2* stats = (uint2*)box;
   uint2* pk = stats + (long)V * W * Hp;
-  dim3 g((W + BS_TW - 1) / BS_TW, (Hp + BS_TH - 1) / BS_TH, V);
+  dim3 g((W + BS_TW - 1) / BS_TW, (Hp + BS_TH - 1) / BS_TH, z1 - z0);
   if (K == 5)
-    hipLaunchKernelGGL(k_box_stats<2>, g, dim3(256), 0, s, l8, W, H, stats, pk);
+    hipLaunchKernelGGL(k_box_stats<2>, g, dim3(256), 0, s, l8, W, H, z0, stats, pk);
   else
-    hipLaunchKernelGGL(k_box_stats<3>, g, dim3(256), 0, s, l8, W, H, stats, pk);
+    hipLaunchKernelGGL(k_box_stats<3>, g, dim3(256), 0, s, l8, W, H, z0, stats, pk);
   MVS_LAUNCH_CHECK("k_box_stats");
   return 0;
 }
@@ -638,22 +647,50 @@ int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, con
     const char* e = getenv("MVS_NCC_NW");
     return e ? atoi(e) : 8;
   }();
+  // per-context override (mvs_set_ncc_variant): the first variant tried
+  const int dpw_pref = ctx->ncc_dpw ? ctx->ncc_dpw : dpw_env;
+  const int nw_pref = ctx->ncc_nw ? ctx->ncc_nw : nw_env;
   int rc = 1;
   // first the widest variant whose double-buffered bands leave room for two
   // workgroups per CU (vertical shifts grow the bands: fewer levels per step
   // then beat a single resident workgroup), then any that fits the LDS
 #define MVS_NCC_TRY(KK, DD, WW)                                                                     \
   if (rc == 1) rc = launch_ncc_t<KK, 8, DD, WW>(ctx, stats, pk, a, levels_host, fdx, fdy, bl, vol, wo, cap);
+  // a variant forced through mvs_set_ncc_variant is tried first, at the full LDS
+  if (ctx->ncc_nw || ctx->ncc_dpw) {
+    const size_t cap = (size_t)160 * 1024;
+    if (K == 5) {
+      if (nw_pref >= 8 && dpw_pref >= 4) {
+        MVS_NCC_TRY(5, 4, 8)
+      } else if (dpw_pref >= 4) {
+        MVS_NCC_TRY(5, 4, 4)
+      } else if (dpw_pref >= 2) {
+        MVS_NCC_TRY(5, 2, 4)
+      } else {
+        MVS_NCC_TRY(5, 1, 4)
+      }
+    } else if (K == 7) {
+      if (nw_pref >= 8 && dpw_pref >= 4) {
+        MVS_NCC_TRY(7, 4, 8)
+      } else if (dpw_pref >= 4) {
+        MVS_NCC_TRY(7, 4, 4)
+      } else if (dpw_pref >= 2) {
+        MVS_NCC_TRY(7, 2, 4)
+      } else {
+        MVS_NCC_TRY(7, 1, 4)
+      }
+    }
+  }
   for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
     if (K == 5) {
-      if (nw_env >= 8 && dpw_env >= 4) MVS_NCC_TRY(5, 4, 8)
-      if (dpw_env >= 4) MVS_NCC_TRY(5, 4, 4)
-      if (dpw_env >= 2) MVS_NCC_TRY(5, 2, 4)
+      if (nw_pref >= 8 && dpw_pref >= 4) MVS_NCC_TRY(5, 4, 8)
+      if (dpw_pref >= 4) MVS_NCC_TRY(5, 4, 4)
+      if (dpw_pref >= 2) MVS_NCC_TRY(5, 2, 4)
       MVS_NCC_TRY(5, 1, 4)
     } else if (K == 7) {
-      if (nw_env >= 8 && dpw_env >= 4) MVS_NCC_TRY(7, 4, 8)
-      if (dpw_env >= 4) MVS_NCC_TRY(7, 4, 4)
-      if (dpw_env >= 2) MVS_NCC_TRY(7, 2, 4)
+      if (nw_pref >= 8 && dpw_pref >= 4) MVS_NCC_TRY(7, 4, 8)
+      if (dpw_pref >= 4) MVS_NCC_TRY(7, 4, 4)
+      if (dpw_pref >= 2) MVS_NCC_TRY(7, 2, 4)
       MVS_NCC_TRY(7, 1, 4)
     } else {
       return arg_fail("NCC window must be 5 or 7");

@@ -174,8 +174,8 @@ __global__ __launch_bounds__(256) void k_init_state(RArgs c, const float* __rest
                                                     const uint32_t* __restrict__ labels,
                                                     const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
                                                     const int* __restrict__ vs, const int* __restrict__ sn, int nks,
-                                                    float kss, float* __restrict__ state) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+                                                    float kss, int z0, float* __restrict__ state) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = z0 + blockIdx.z;
   if (x >= c.mw) return;
   long M = (long)c.mw * c.mh;
   long idx = M * z + (long)c.mw * y + x;
@@ -693,9 +693,9 @@ __global__ void k_spixl_to_image(const float* __restrict__ spixl, const uint32_t
 }
 
 // ---- cross-view filter -------------------------------------------------------
-__global__ void k_proj_inv(const float* __restrict__ full, int V, int W, int H, int aw, float bl,
+__global__ void k_proj_inv(const float* __restrict__ full, int V, int W, int H, int aw, float bl, int z0,
                            float* __restrict__ proj) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = blockIdx.z;
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
   if (x >= W) return;
   long P = (long)W * H, p = (long)y * W + x;
   int crx = r % aw, cry = r / aw;
@@ -929,10 +929,12 @@ int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, fl
 
 int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
                       const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
-                      const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state) {
+                      const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state,
+                      int z0, int z1) {
+  if (z1 <= z0) return 0;
   RArgs c{V, W, H, S, map_dim(W, S), map_dim(H, S), aw, bl, fuse, alpha, gamma};
-  hipLaunchKernelGGL(k_init_state, dim3((c.mw + 63) / 64, c.mh, V), dim3(64), 0, s, c, spixl, labels, rep,
-                     (const float2*)flat, vs, sn, nks, kss, state);
+  hipLaunchKernelGGL(k_init_state, dim3((c.mw + 63) / 64, c.mh, z1 - z0), dim3(64), 0, s, c, spixl, labels, rep,
+                     (const float2*)flat, vs, sn, nks, kss, z0, state);
   MVS_LAUNCH_CHECK("k_init_state");
   return 0;
 }
@@ -959,10 +961,20 @@ int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float
   return 0;
 }
 
-int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
-                  float* proj, float* out, int z0, int z1) {
-  hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, H, V), dim3(256), 0, s, full, V, W, H, aw, bl, proj);
+// project_to_reference_inv for reference views [z0, z1): proj slices z0..z1-1
+int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const float* full, float* proj, int z0,
+                    int z1) {
+  if (z1 <= z0) return 0;
+  hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, H, z1 - z0), dim3(256), 0, s, full, V, W, H, aw, bl, z0,
+                     proj);
   MVS_LAUNCH_CHECK("k_proj_inv");
+  return 0;
+}
+
+// remove_view_inconsistency for reference views [z0, z1): reads every proj
+// slice (all V must be filled) and the full disparity stack
+int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
+                         const float* proj, float* out, int z0, int z1) {
   if (z1 > z0) {
     const dim3 g((W + 255) / 256, H, z1 - z0);
     const dim3 gp((W + 255) / 256, H);
@@ -981,6 +993,14 @@ int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fu
     MVS_LAUNCH_CHECK("k_remove_incons");
   }
   return 0;
+}
+
+// pinned order: every projection, then the removal
+int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
+                  float* proj, float* out, int z0, int z1) {
+  int rc = launch_proj_inv(s, V, W, H, aw, bl, full, proj, 0, V);
+  if (rc) return rc;
+  return launch_remove_incons(s, V, W, H, aw, bl, fuse, full, proj, out, z0, z1);
 }
 
 }  // namespace mvs

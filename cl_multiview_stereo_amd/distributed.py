@@ -8,24 +8,33 @@ exchange exactly what later stages read from other views:
 
   stage                             reads from other views    exchange
   --------------------------------  ------------------------  ---------------------------
-  cvt (a1)                          -                         none (every rank holds the
-                                                              RGBx stack, converts all)
+  cvt (a1), block + its neighbours  -                         none (every rank holds the
+                                                              RGBx stack; converts only
+                                                              the views its block reads)
   SLIC (a2-a6), own block           -                         all-gather spixl + labels
-  boundary (a8)                     -                         none (cheap, all views)
+  boundary (a8), own block          -                         none
   superpixel sweep (a9), own block  Lab of neighbours         all-gather spixl (s7 = seed)
-  per-pixel NCC + WTA, own block    l8 of neighbours          none until the filter
-  flatness / init state (a11-a12)   neighbours' s7 / labels   none (recomputed redundantly)
+  per-pixel NCC + WTA, own block    l8 / window planes of     none until the filter
+                                    neighbours (built for the
+                                    block + neighbours only)
+  flatness (a11)                    -                         none (all views, a few us)
+  init state (a12), own block       neighbours' s7 / labels   all-gather state (S=32:
+                                                              49 KB/view)
   propagate (a13) x no_prop         neighbours' state         all-gather state every
-                                                              iteration (49 KB/view at S=32)
+                                                              iteration
   fusion (a14), own block           -                         -
-  cross-view filter (a15)           all disparity maps        ONE all-gather of disparity
+  projection (a15 i), own block     all disparity maps        all-gather disparity, then
+                                                              all-gather proj
+  removal (a15 ii), own block       all proj slices, all      -
+                                    disparity maps
 
 The backend does the compute for one rank: ``EngineBackend`` (HIP kernels
 through libmvs.so) on a GPU.  The tests substitute a CPU stand-in of the same
 interface, so that this orchestration runs under gloo with world_size 2.
-The collectives use ``all_gather_into_tensor``, which is RCCL on ROCm, for
-equal blocks, and fall back to list all-gather when blocks are ragged (or on
-gloo).
+The collectives use ``all_gather_into_tensor`` (RCCL on ROCm; gloo also
+implements it, so the CPU tests run the same branch) for equal blocks, in
+place when the local block is a slice of the full tensor, and fall back to a
+padded list all-gather when blocks are ragged.
 """
 from __future__ import annotations
 
@@ -55,9 +64,9 @@ def all_blocks(V: int, world: int) -> list[tuple[int, int]]:
 class ViewGather:
     """All-gather of per-view blocks along dim 0 into a full [V, ...] tensor.
 
-    With equal blocks on an RCCL group this is one ``all_gather_into_tensor``
-    (in place when `full` is given).  Ragged blocks (V % world != 0) and gloo
-    use the list form."""
+    With equal blocks this is one ``all_gather_into_tensor`` (in place when
+    `local` is `full`'s own block).  Ragged blocks (V % world != 0) use the
+    padded list form."""
 
     def __init__(self, V: int, group=None):
         self.V = V
@@ -83,7 +92,7 @@ class ViewGather:
             if full.data_ptr() != local.data_ptr():
                 full.copy_(local)
             return full
-        if self.equal and self.backend == "nccl":
+        if self.equal:
             src = local if local.is_contiguous() else local.contiguous()
             dist.all_gather_into_tensor(full, src, group=self.group)
             return full
@@ -127,80 +136,94 @@ class ShardedPipeline:
             raise ValueError("stack size does not match the gather's view count")
         z0, z1 = g.block
         S = st.spixl_size
-        lab, l8 = b.cvt(rgbx)
+        need = self.cam.views_needed(z0, z1)
+        lab, l8 = b.cvt(rgbx, need)
         sp_blk, lb_blk = b.slic(lab[z0:z1], S, st.slic_color_weight, st.no_iter, st.enforce_connectivity)
         spixl = g(sp_blk)
         labels = g(lb_blk)
-        rep = b.boundary(spixl, labels, S)
+        rep = b.boundary(spixl, labels, S, z0, z1)
         b.sweep_spixl(lab, spixl, rep, self.cam, S, z0, z1)
-        spixl = g(spixl[z0:z1].contiguous(), spixl)
+        spixl = g(spixl[z0:z1], spixl)
         out = ShardOutput(z0, z1, spixl, labels)
         if self.pixel_cost:
-            out.disp, out.conf = b.pixel_sweep(lab, l8, self.cam, z0, z1, self.pixel_cost, st.window)
+            out.disp, out.conf = b.pixel_sweep(lab, l8, self.cam, z0, z1, self.pixel_cost, st.window, need)
         if self.refine:
             out.disp_refined = self._refine(spixl, labels, rep, z0, z1)
         if self.filt:
             src = out.disp_refined if out.disp_refined is not None else out.disp
             full = g(src)
-            out.disp_filtered = b.filter(full, st.array_width, st.bl_ratio, st.fuse, z0, z1)[z0:z1]
+            # project_to_reference_inv for the block, then every rank holds all
+            # proj slices, which remove_view_inconsistency reads (clcode.cl:2054)
+            proj = b.proj_inv(full, st.array_width, st.bl_ratio, z0, z1)
+            g(proj[z0:z1], proj)
+            out.disp_filtered = b.remove_inconsistency(full, proj, st.array_width, st.bl_ratio, st.fuse, z0, z1)[z0:z1]
         return out
 
     def _refine(self, spixl, labels, rep, z0, z1):
         """clDepthRefinement::do_refinement (depth_refinement.cpp:91-118, 724-889)
-        with the Jacobi ping-pong of mvs_refine_d; each iteration's output block
-        is all-gathered before the next iteration reads it."""
+        with the Jacobi ping-pong of mvs_refine_d: the block's initial state
+        and each iteration's output block are all-gathered before the next
+        iteration reads the neighbours' states."""
         st, b, g = self.st, self.b, self.g
         rp = params.refine_params(st)
         flat = b.flatness(spixl, rp["flat_gamma"])
         state = b.init_state(spixl, labels, rep, flat, self.cam, st.spixl_size, rp["init_gamma"], rp["init_alpha"],
-                             rp["kernel_steps"], rp["kss"], rp["fuse"])
+                             rp["kernel_steps"], rp["kss"], rp["fuse"], z0, z1)
+        g(state[z0:z1], state)
         state2 = state.clone()
         for it in range(st.no_prop):
             src, dst = (state, state2) if it % 2 == 0 else (state2, state)
             nks, kss = params.prop_schedule(it, rp["kernel_steps"], rp["kss"])
             b.propagate(spixl, labels, rep, flat, self.cam, st.spixl_size, it, rp["prop_alpha"], rp["prop_gamma"],
                         rp["fuse"], nks, kss, src, dst, z0, z1)
-            g(dst[z0:z1].contiguous(), dst)
+            g(dst[z0:z1], dst)
         # fusion renders current_state_dev = `state` (Appendix A #13)
         return b.spixl_to_image(spixl[z0:z1], labels[z0:z1], state[z0:z1], st.spixl_size)
 
 
 class EngineBackend:
     """Per-rank compute on the GPU through libmvs.so (Engine).  fused: the per-pixel
-    NCC sweep folds its winner-take-all in (no cost volume; same maps)."""
+    NCC sweep folds its winner-take-all in (no cost volume; same maps).
+    Buffers that only the listed views fill (Lab, l8, window planes, rep,
+    state) are full-size [V, ...] so kernels index them by global view id."""
 
     def __init__(self, engine, fused: bool = False):
         self.e, self.fused = engine, fused
         self._sweeps = {}  # PixelSweep (volume buffers, side stream) per configuration
 
-    def cvt(self, rgbx):
-        return self.e.cvt(rgbx, want_l8=True)
+    def cvt(self, rgbx, views):
+        V, H, W, _ = rgbx.shape
+        lab = self.e.empty((V, H, W, 4), torch.float32)
+        l8 = self.e.empty((V, H, W), torch.uint8)
+        return self.e.cvt_views(rgbx, views, lab, l8)
 
     def slic(self, lab_blk, S, weight, no_iter, conn):
         if S == 1:
             return self.e.grid(lab_blk, 1)
         return self.e.slic(lab_blk, S, weight, no_iter, conn)
 
-    def boundary(self, spixl, labels, S):
-        return self.e.boundary(spixl, labels, S)
+    def boundary(self, spixl, labels, S, z0, z1):
+        rep = torch.zeros(tuple(spixl.shape[:3]) + (8,), dtype=torch.uint8, device=self.e.device)
+        rep[z0:z1] = self.e.boundary(spixl[z0:z1], labels[z0:z1], S)
+        return rep
 
     def sweep_spixl(self, lab, spixl, rep, cam, S, z0, z1):
         self.e.sweep_spixl(lab, spixl, rep, cam, S, z0, z1)
 
-    def pixel_sweep(self, lab, l8, cam, z0, z1, cost, K):
+    def pixel_sweep(self, lab, l8, cam, z0, z1, cost, K, views):
         from .pipeline import PixelSweep
         H, W = lab.shape[1:3]
         key = (id(cam), W, H, cost, K)
         ps = self._sweeps.get(key)
         if ps is None:
             ps = self._sweeps[key] = PixelSweep(self.e, cam, W, H, cost, K, self.fused)
-        return ps.run(lab, l8, z0, z1)
+        return ps.run(lab, l8, z0, z1, views=views)
 
     def flatness(self, spixl, gamma):
         return self.e.flatness(spixl, gamma)
 
-    def init_state(self, *a):
-        return self.e.init_state(*a)
+    def init_state(self, spixl, labels, rep, flat, cam, S, gamma, alpha, nks, kss, fuse, z0, z1):
+        return self.e.init_state_range(spixl, labels, rep, flat, cam, S, gamma, alpha, nks, kss, fuse, z0, z1)
 
     def propagate(self, *a):
         return self.e.propagate(*a)
@@ -208,8 +231,11 @@ class EngineBackend:
     def spixl_to_image(self, spixl, labels, state, S):
         return self.e.spixl_to_image(spixl.contiguous(), labels.contiguous(), state.contiguous(), S)
 
-    def filter(self, disp_full, aw, bl, fuse, z0, z1):
-        return self.e.filter(disp_full, aw, bl, fuse, z0, z1)[1]
+    def proj_inv(self, disp_full, aw, bl, z0, z1):
+        return self.e.proj_inv(disp_full, aw, bl, z0, z1)
+
+    def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1):
+        return self.e.remove_inconsistency(disp_full, proj, aw, bl, fuse, z0, z1)
 
 
 def init_from_env(backend: str = "nccl"):

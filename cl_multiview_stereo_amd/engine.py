@@ -31,6 +31,18 @@ def _ptr(t: torch.Tensor | None):
     return C.c_void_p(t.data_ptr())
 
 
+def _runs(views):
+    """Sorted view ids -> contiguous [v0, v1) runs."""
+    vs = sorted(set(int(v) for v in views))
+    runs = []
+    for v in vs:
+        if runs and runs[-1][1] == v:
+            runs[-1][1] = v + 1
+        else:
+            runs.append([v, v + 1])
+    return [tuple(r) for r in runs]
+
+
 @dataclass
 class CameraArray:
     """Host-side camera-array metadata (pipeline::perform_depth_est)."""
@@ -57,6 +69,14 @@ class CameraArray:
     @property
     def D(self) -> int:
         return int(self.levels.shape[0])
+
+    def views_needed(self, z0: int, z1: int) -> list[int]:
+        """Reference views [z0, z1) and every view their neighbour lists name:
+        the views whose images a shard owning [z0, z1) reads."""
+        need = set(range(z0, z1))
+        for z in range(z0, z1):
+            need.update(int(v) for v in self.view_subset[z, :int(self.subset_num[z])])
+        return sorted(need)
 
     def desc(self):
         return C.byref(self._desc)
@@ -100,6 +120,16 @@ class Engine:
         l8 = self.empty((V, H, W), torch.uint8) if want_l8 else None
         self._stream()
         _lib.check(self.L.mvs_cvt_d(self.ctx, _ptr(rgbx), V, W, H, _ptr(lab), _ptr(l8)), "mvs_cvt_d")
+        return lab, l8
+
+    def cvt_views(self, rgbx: torch.Tensor, views, lab: torch.Tensor, l8: torch.Tensor | None = None):
+        """cvt of the listed views only, into full-size [V, ...] lab / l8 (a view
+        shard converts its block and the block's neighbours)."""
+        V, H, W, _ = rgbx.shape
+        self._stream()
+        for v0, v1 in _runs(views):
+            _lib.check(self.L.mvs_cvt_d(self.ctx, _ptr(rgbx[v0:v1]), v1 - v0, W, H, _ptr(lab[v0:v1]),
+                                        None if l8 is None else _ptr(l8[v0:v1])), "mvs_cvt_d")
         return lab, l8
 
     def slic(self, lab: torch.Tensor, S: int, weight: float = 0.6, no_iter: int = 5, enforce_connectivity=False,
@@ -162,6 +192,25 @@ class Engine:
         self._stream()
         _lib.check(self.L.mvs_box_stats_d(self.ctx, _ptr(l8), V, W, H, K, _ptr(out)), "mvs_box_stats_d")
         return out
+
+    def box_stats_views(self, l8, K: int, views, out):
+        """Window planes of the listed views only, into a full V-view buffer."""
+        V, H, W = l8.shape
+        self._stream()
+        for v0, v1 in _runs(views):
+            _lib.check(self.L.mvs_box_stats_range_d(self.ctx, _ptr(l8), V, W, H, K, v0, v1, _ptr(out)),
+                       "mvs_box_stats_range_d")
+        return out
+
+    def set_ncc_variant(self, waves: int = 0, levels_per_wave: int = 0, band_w: int = 0, general_rows: bool = False):
+        """Force the NCC sweep variant tried first (0 = automatic; test / tuning hook)."""
+        _lib.check(self.L.mvs_set_ncc_variant(self.ctx, int(waves), int(levels_per_wave), int(band_w),
+                                              int(bool(general_rows))), "mvs_set_ncc_variant")
+
+    def ncc_last_variant(self) -> dict:
+        v = (C.c_int32 * 7)()
+        _lib.check(self.L.mvs_ncc_last_variant(self.ctx, v), "mvs_ncc_last_variant")
+        return dict(zip(("K", "TH", "DPW", "NW", "BW", "EVEN", "FUSE"), list(v)))
 
     def ncc_volume(self, l8, box, cam: CameraArray, z: int, K: int = 5, out=None):
         V, H, W = l8.shape
@@ -237,6 +286,19 @@ class Engine:
                                            C.c_float(fuse), _ptr(st)), "mvs_init_state_d")
         return st
 
+    def init_state_range(self, spixl, labels, rep, flat, cam: CameraArray, S, gamma, alpha, nks, kss, fuse, z0, z1,
+                         state=None):
+        """init_current_state for views [z0, z1) into a full [V, mh, mw, 6] state."""
+        V, H, W = labels.shape
+        mw, mh = map_size(W, H, S)
+        st = self.empty((V, mh, mw, 6), torch.float32) if state is None else state
+        self._stream()
+        _lib.check(self.L.mvs_init_state_range_d(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), _ptr(flat),
+                                                 cam.desc(), C.c_float(gamma), C.c_float(alpha), int(nks),
+                                                 C.c_float(kss), C.c_float(fuse), int(z0), int(z1), _ptr(st)),
+                   "mvs_init_state_range_d")
+        return st
+
     def propagate(self, spixl, labels, rep, flat, cam: CameraArray, S, it, alpha, gamma, fuse, nks, kss, st_in,
                   st_out, z0=0, z1=None):
         V, H, W = labels.shape
@@ -266,6 +328,26 @@ class Engine:
         _lib.check(self.L.mvs_filter_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio), C.c_float(fuse),
                                        _ptr(disp_full), _ptr(proj), _ptr(out), int(z0), int(z1)), "mvs_filter_d")
         return proj, out
+
+    def proj_inv(self, disp_full, array_width: int, bl_ratio: float, z0: int, z1: int, proj=None):
+        """project_to_reference_inv for references [z0, z1) into proj[z0:z1] ([V, H, W])."""
+        V, H, W = disp_full.shape
+        proj = self.empty((V, H, W), torch.float32) if proj is None else proj
+        self._stream()
+        _lib.check(self.L.mvs_proj_inv_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio), _ptr(disp_full),
+                                         _ptr(proj), int(z0), int(z1)), "mvs_proj_inv_d")
+        return proj
+
+    def remove_inconsistency(self, disp_full, proj, array_width: int, bl_ratio: float, fuse: float, z0: int, z1: int,
+                             out=None):
+        """remove_view_inconsistency for references [z0, z1) (every proj slice filled)."""
+        V, H, W = disp_full.shape
+        out = torch.zeros((V, H, W), dtype=torch.float32, device=self.device) if out is None else out
+        self._stream()
+        _lib.check(self.L.mvs_remove_inconsistency_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio),
+                                                     C.c_float(fuse), _ptr(disp_full), _ptr(proj), _ptr(out),
+                                                     int(z0), int(z1)), "mvs_remove_inconsistency_d")
+        return out
 
     def synchronize(self):
         _lib.check(self.L.mvs_synchronize(self.ctx), "mvs_synchronize")

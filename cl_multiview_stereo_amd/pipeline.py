@@ -72,7 +72,9 @@ class PixelSweep:
             self.vol = engine.empty((cam.D, H, W), torch.float32)
         self.levels = engine.levels_dev(cam)
 
-    def run(self, lab, l8, z0: int, z1: int, disp_out=None, conf_out=None):
+    def run(self, lab, l8, z0: int, z1: int, disp_out=None, conf_out=None, views=None):
+        """Reference views [z0, z1).  views: the views whose window planes are
+        built (default all; a view shard passes its block + neighbours)."""
         n = z1 - z0
         disp = self.e.empty((n, self.H, self.W), torch.float32) if disp_out is None else disp_out
         conf = None
@@ -80,7 +82,11 @@ class PixelSweep:
             self.e.sweep_pixel_sad(lab, self.cam, z0, z1, out=disp)
             return disp, None
         conf = self.e.empty((n, self.H, self.W), torch.float32) if conf_out is None else conf_out
-        box = self.e.box_stats(l8, self.K)
+        if views is None:
+            box = self.e.box_stats(l8, self.K)
+        else:
+            V, H, W = l8.shape
+            box = self.e.box_stats_views(l8, self.K, views, self.e.empty((2, V, H + (H & 1), W, 2), torch.int32))
         for i, z in enumerate(range(z0, z1)):
             if self.fused:
                 self.e.ncc_wta(l8, box, self.cam, z, self.K, disp=disp[i], conf=conf[i])

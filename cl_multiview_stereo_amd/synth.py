@@ -63,8 +63,11 @@ def render_stack(tex: np.ndarray, disp: np.ndarray, array_width: int, array_heig
         ok = (tx >= 0) & (tx < W) & (ty >= 0) & (ty < H)
         flat = (ty * W + tx)[ok]
         dd = disp[ok]
+        # z-buffer (max disparity per target pixel): scatter the few distinct
+        # disparities in increasing order, so the largest lands last
         z = np.full(H * W, -1, np.int64)
-        np.maximum.at(z, flat, dd)
+        for dv in np.unique(dd):
+            z[flat[dd == dv]] = dv
         win = dd == z[flat]
         img = rng.integers(0, 256, size=(H * W, 3), dtype=np.uint8)  # holes -> noise
         img[flat[win]] = tex.reshape(-1, 3)[np.flatnonzero(ok)[win]]

@@ -126,6 +126,10 @@ int mvs_sweep_pixel_sad_d(mvs_ctx* ctx, int W, int H, const float* lab, const mv
  * vol [D][H][W] float cost of reference view z = 1 - max(-1, best NCC over
  * valid neighbour windows); l8 is validated only. */
 int mvs_box_stats_d(mvs_ctx* ctx, const uint8_t* l8, int V, int W, int H, int K, int32_t* box);
+/* The same planes for views [z0, z1) only of a V-view box buffer (a view shard
+ * converts just its block and the block's neighbours). */
+int mvs_box_stats_range_d(mvs_ctx* ctx, const uint8_t* l8, int V, int W, int H, int K, int z0, int z1,
+                          int32_t* box);
 int mvs_ncc_volume_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
                      int K, int z, float* vol);
 /* Winner-take-all over vol [D][H][W]: disp = levels[first argmin], conf =
@@ -136,6 +140,15 @@ int mvs_wta_d(mvs_ctx* ctx, int W, int H, int D, const float* vol, const float* 
  * conf may be NULL. */
 int mvs_ncc_wta_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
                   int K, int z, float* disp, float* conf);
+/* Tuning / test hook: the NCC sweep variant this context tries first (0 =
+ * automatic): waves per workgroup 4|8, levels per wave 1|2|4 (8 waves: 4),
+ * minimum LDS band width 128|192|256 columns, general_rows 1 = the kernel
+ * that handles band rows starting on either row parity even when all start
+ * on a pair.  Variants that do not fit the LDS fall back as in the default
+ * chain.  mvs_ncc_last_variant reports the last launch as
+ * {K, TH, levels per wave, waves, band width, even rows, fused}. */
+int mvs_set_ncc_variant(mvs_ctx* ctx, int waves, int levels_per_wave, int band_w, int general_rows);
+int mvs_ncc_last_variant(mvs_ctx* ctx, int32_t* out7);
 
 /* Superpixel-plane refinement (clDepthRefinement, depth_refinement.cpp:91-1470).
  * flat [V][mh][mw][2] and state/state2 [V][mh][mw][6] are caller-provided
@@ -144,6 +157,10 @@ int mvs_flatness_d(mvs_ctx* ctx, int V, int mw, int mh, const float* spixl, floa
 int mvs_init_state_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
                      const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
                      int kernel_steps, float kss, float fuse, float* state);
+/* init_current_state for views [z0, z1) only (state rows of other views untouched). */
+int mvs_init_state_range_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
+                           const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
+                           int kernel_steps, float kss, float fuse, int z0, int z1, float* state);
 int mvs_propagate_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
                     const uint8_t* rep, const float* flat, const mvs_array* a, int iter, float alpha,
                     float gamma, float fuse, int kernel_steps, float kss, const float* st_in, float* st_out,
@@ -159,6 +176,15 @@ int mvs_refine_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const ui
  * reference views [z0, z1).  proj/out [V][H][W]. */
 int mvs_filter_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, float fuse,
                  const float* disp_full, float* proj, float* out, int z0, int z1);
+/* The filter's two passes separately, for view sharding: project_to_reference_inv
+ * (clcode.cl:1995-2034) writes proj slices [z0, z1); remove_view_inconsistency
+ * (clcode.cl:2037-2101) for references [z0, z1) reads EVERY proj slice, so a
+ * shard all-gathers proj in between.  mvs_filter_d == proj_inv(0, V) +
+ * remove_inconsistency(z0, z1). */
+int mvs_proj_inv_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, const float* disp_full,
+                   float* proj, int z0, int z1);
+int mvs_remove_inconsistency_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, float fuse,
+                               const float* disp_full, const float* proj, float* out, int z0, int z1);
 
 /* ---- host-pointer stage API (mirrors the reference stage methods) ------- */
 /* clSLIC::do_super_pixel_seg(in_img, lab_out, spixl_out, idx_out), one view. */

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export OMP_NUM_THREADS=${OMP_NUM_THREADS:-16}
-timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 ${PYTEST_ARGS:-} \
+timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
   > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -40 gpurun_out/gpu_tests.log

@@ -15,9 +15,16 @@ def _np(t):
 
 
 class OracleBackend:
-    def cvt(self, rgbx):
-        lab = orc.cvt(_np(rgbx))
-        return torch.from_numpy(lab), torch.from_numpy(orc.l8(lab))
+    def cvt(self, rgbx, views):
+        # only the listed views are converted; the rest stay NaN / 0xff so a
+        # stage reading a view outside its block's needs shows up as a mismatch
+        x = _np(rgbx)
+        lab = np.full(x.shape, np.nan, np.float32)
+        q = np.full(x.shape[:3], 255, np.uint8)
+        for v in views:
+            lab[v] = orc.cvt(x[v])
+            q[v] = orc.l8(lab[v])
+        return torch.from_numpy(lab), torch.from_numpy(q)
 
     def slic(self, lab_blk, S, weight, no_iter, conn):
         lab = _np(lab_blk)
@@ -26,15 +33,17 @@ class OracleBackend:
         lb = np.stack([o[1] for o in outs]).view(np.int32)
         return torch.from_numpy(sp), torch.from_numpy(lb)
 
-    def boundary(self, spixl, labels, S):
-        return torch.from_numpy(orc.boundary(_np(spixl), _np(labels).view(np.uint32), S))
+    def boundary(self, spixl, labels, S, z0, z1):
+        rep = np.full(tuple(spixl.shape[:3]) + (8,), 255, np.uint8)
+        rep[z0:z1] = orc.boundary(_np(spixl)[z0:z1], _np(labels).view(np.uint32)[z0:z1], S)
+        return torch.from_numpy(rep)
 
     def sweep_spixl(self, lab, spixl, rep, cam, S, z0, z1):
         sp = orc.sweep(_np(lab), _np(spixl), _np(rep), cam.levels, cam.view_subset, cam.subset_num,
                        cam.array_width, cam.bl_ratio, S, z0, z1)
         spixl.copy_(torch.from_numpy(sp))
 
-    def pixel_sweep(self, lab, l8, cam, z0, z1, cost, K):
+    def pixel_sweep(self, lab, l8, cam, z0, z1, cost, K, views):
         if cost == "sad":
             d = orc.sweep_pixel_sad(_np(lab), cam.levels, cam.view_subset, cam.subset_num, cam.array_width,
                                     cam.bl_ratio, z0, z1)
@@ -51,10 +60,14 @@ class OracleBackend:
     def flatness(self, spixl, gamma):
         return torch.from_numpy(orc.flatness(_np(spixl), gamma))
 
-    def init_state(self, spixl, labels, rep, flat, cam, S, gamma, alpha, nks, kss, fuse):
-        return torch.from_numpy(orc.init_state(_np(spixl), _np(labels).view(np.uint32), _np(rep), _np(flat),
-                                               cam.view_subset, cam.subset_num, cam.array_width, cam.bl_ratio, S,
-                                               gamma, alpha, nks, kss, fuse))
+    def init_state(self, spixl, labels, rep, flat, cam, S, gamma, alpha, nks, kss, fuse, z0, z1):
+        r = np.zeros_like(_np(rep))  # the oracle runs every view: give the others harmless extents
+        r[z0:z1] = _np(rep)[z0:z1]
+        st = orc.init_state(_np(spixl), _np(labels).view(np.uint32), r, _np(flat), cam.view_subset,
+                            cam.subset_num, cam.array_width, cam.bl_ratio, S, gamma, alpha, nks, kss, fuse)
+        out = np.full(st.shape, np.nan, np.float32)
+        out[z0:z1] = st[z0:z1]
+        return torch.from_numpy(out)
 
     def propagate(self, spixl, labels, rep, flat, cam, S, it, alpha, gamma, fuse, nks, kss, st_in, st_out, z0, z1):
         out = orc.propagate(_np(spixl), _np(labels).view(np.uint32), _np(rep), _np(flat), cam.view_subset,
@@ -66,8 +79,18 @@ class OracleBackend:
     def spixl_to_image(self, spixl, labels, state, S):
         return torch.from_numpy(orc.spixl_to_image(_np(spixl), _np(labels).view(np.uint32), _np(state), S))
 
-    def filter(self, disp_full, aw, bl, fuse, z0, z1):
-        _, out = orc.filt(_np(disp_full), aw, bl, fuse)
+    def proj_inv(self, disp_full, aw, bl, z0, z1):
+        proj, _ = orc.filt(_np(disp_full), aw, bl, 1.0)
+        out = np.full(proj.shape, np.nan, np.float32)
+        out[z0:z1] = proj[z0:z1]
+        return torch.from_numpy(out)
+
+    def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1):
+        # the oracle filter recomputes every projection itself: check that the
+        # gathered proj the product orchestration hands over equals it
+        oproj, out = orc.filt(_np(disp_full), aw, bl, fuse)
+        if not np.array_equal(_np(proj).view(np.uint32), oproj.view(np.uint32)):
+            raise AssertionError("gathered proj slices differ from the full projection")
         res = torch.zeros_like(disp_full)
         res[z0:z1] = torch.from_numpy(out[z0:z1])
         return res

@@ -1,0 +1,189 @@
+"""GPU parity of the NCC sweep at the BASELINE configurations' own geometry,
+and of every kernel instantiation, against the oracle (orc_ncc_volume /
+orc_wta, oracle/mvs_oracle.c).
+
+* C5 (5x1 array, NCC 7x7, levels 0..255, 4096 columns): the neighbours are
+  horizontal, so a row band of the full-width image carries the full image's
+  arithmetic; the full 4096x3072x256 volume (3.22 G cells, past 2^31) is then
+  checked on bands at the top, middle and bottom against the oracle run on the
+  band's rows (the band's rows R away from its cut edges equal the full image's).
+* C4 (8x4 array, 5 nearest neighbours, 128 levels): vertical and diagonal
+  neighbours, whose taller LDS bands select the narrower variants.
+* Every (K, levels per wave, waves, band width, row parity, fused) variant,
+  forced per call through mvs_set_ncc_variant.
+Bar: bit-exact (costs, disparities, confidences)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from cl_multiview_stereo_amd import params, synth
+from cl_multiview_stereo_amd.engine import CameraArray
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    a = a.cpu().numpy() if hasattr(a, "cpu") else np.asarray(a)
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def same(a, b, what):
+    a, b = bits(a), bits(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    bad = np.count_nonzero(a != b)
+    assert bad == 0, f"{what}: {bad}/{a.size} differ, first at {np.argwhere(a != b)[:3].tolist()}"
+
+
+@pytest.fixture
+def eng(engine):
+    engine.set_ncc_variant()
+    yield engine
+    engine.set_ncc_variant()  # back to automatic for the other tests
+
+
+def _array(aw, ah, dmin, dmax, nh=0, nv=0, knn=None, bl=1.0):
+    levels = params.disparity_levels(dmin, dmax, 1)
+    lists = params.nearest_neighbours(aw, ah, knn) if knn else params.neighbour_lists(aw, ah, nh, nv)
+    vs, sn = params.flatten_subsets(lists)
+    return CameraArray(aw, bl, levels, vs, sn)
+
+
+def _check_view(eng, l8, box, cam, z, K, want_vol=None, rows=None):
+    """GPU volume / WTA / fused sweep of reference view z against the oracle
+    (rows: compare only these rows, the oracle having run on the same rows)."""
+    l8h = l8.cpu().numpy()
+    want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, cam.array_width, cam.bl_ratio, K, z) \
+        if want_vol is None else want_vol
+    od, oc = orc.wta(want, cam.levels)
+    vol = eng.ncc_volume(l8, box, cam, z, K)
+    sl = slice(None) if rows is None else rows
+    same(vol[:, sl], want[:, sl], f"volume z{z} K{K}")
+    disp, conf = eng.wta(vol, eng.levels_dev(cam))
+    same(disp[sl], od[sl], f"wta disp z{z}")
+    same(conf[sl], oc[sl], f"wta conf z{z}")
+    fd, fc = eng.ncc_wta(l8, box, cam, z, K)
+    same(fd[sl], od[sl], f"fused disp z{z}")
+    same(fc[sl], oc[sl], f"fused conf z{z}")
+    del vol
+
+
+def test_c5_band_full_width(eng):
+    """C5's combination on a 64-row band of the full 4096-column image:
+    NCC 7x7, 256 levels, horizontal neighbours up to 4 views away (shifts up
+    to 1020 columns)."""
+    stack, _ = synth.make_stack(4096, 64, 5, 1, 0, 255, 1.0, 0x5EED + 5)
+    cam = _array(5, 1, 0, 255, nh=4)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    box = eng.box_stats(l8, 7)
+    for z in (0, 2, 4):
+        _check_view(eng, l8, box, cam, z, 7)
+    seen = eng.ncc_last_variant()
+    assert seen["K"] == 7 and seen["FUSE"] == 1
+
+
+def test_c5_full_size_bands(eng):
+    """The full C5 size (4096x3072, 256 levels: the volume has 3.22 G cells,
+    indices past 2^31 from level 171 on) against the oracle on three row
+    bands, every level of the band's rows."""
+    W, H, K, R = 4096, 3072, 7, 3
+    stack, _ = synth.make_stack(W, H, 5, 1, 0, 255, 1.0, 0x5EED + 5)
+    cam = _array(5, 1, 0, 255, nh=4)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    del lab
+    box = eng.box_stats(l8, K)
+    z = 2
+    vol = eng.ncc_volume(l8, box, cam, z, K)
+    disp, conf = eng.wta(vol, eng.levels_dev(cam))
+    fd, fc = eng.ncc_wta(l8, box, cam, z, K)
+    torch.cuda.synchronize()
+    same(fd, disp, "fused == two-pass disparity (full size)")
+    same(fc, conf, "fused == two-pass confidence (full size)")
+    l8h = l8.cpu().numpy()
+    for y0, y1 in ((0, 64), (2000, 2064), (H - 64, H)):
+        c0, c1 = max(0, y0 - R), min(H, y1 + R)  # crop whose rows y0..y1-1 see the full image's windows
+        want = orc.ncc_volume(np.ascontiguousarray(l8h[:, c0:c1]), cam.levels, cam.view_subset, cam.subset_num,
+                              5, 1.0, K, z)
+        rows = slice(y0 - c0, y1 - c0)
+        same(vol[:, y0:y1], want[:, rows], f"volume rows {y0}..{y1}")
+        od, oc = orc.wta(want, cam.levels)
+        same(disp[y0:y1], od[rows], f"disp rows {y0}..{y1}")
+        same(conf[y0:y1], oc[rows], f"conf rows {y0}..{y1}")
+        same(fd[y0:y1], od[rows], f"fused disp rows {y0}..{y1}")
+
+
+@pytest.mark.parametrize("bl", [1.0, 1.0359])
+def test_c4_geometry(eng, bl):
+    """C4's array (8x4, 5 nearest neighbours: horizontal, vertical and
+    diagonal) at 128 levels on a cropped image.  The taller bands of the
+    vertical neighbours must select the 2- and 1-level-per-wave variants the
+    full-size C4 run uses, and all of them must match the oracle."""
+    aw, ah, W, H = 8, 4, 256, 72
+    stack, _ = synth.make_stack(W, H, aw, ah, 0, 127, bl, 0x5EED + 4)
+    cam = _array(aw, ah, 0, 127, knn=5, bl=bl)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    l8h = l8.cpu().numpy()
+    box = eng.box_stats(l8, 5)
+    variants = set()
+    for z in range(aw * ah):
+        want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, bl, 5, z)
+        od, oc = orc.wta(want, cam.levels)
+        vol = eng.ncc_volume(l8, box, cam, z, 5)
+        v = eng.ncc_last_variant()
+        variants.add((v["DPW"], v["NW"], v["BW"], v["EVEN"]))
+        same(vol, want, f"volume z{z}")
+        d, c = eng.wta(vol, eng.levels_dev(cam))
+        same(d, od, f"disp z{z}")
+        same(c, oc, f"conf z{z}")
+        fd, fc = eng.ncc_wta(l8, box, cam, z, 5)
+        same(fd, od, f"fused disp z{z}")
+        same(fc, oc, f"fused conf z{z}")
+    dpws = {v[0] for v in variants}
+    assert dpws & {1, 2}, f"C4 geometry should need a narrower variant, saw {sorted(variants)}"
+
+
+_VARIANTS = [(8, 4), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation of the chain
+
+
+@pytest.mark.parametrize("K", [5, 7])
+@pytest.mark.parametrize("geom", ["horizontal", "vertical"])
+def test_every_ncc_variant(eng, K, geom):
+    """Force each (waves, levels per wave) x band width x row-parity variant,
+    plain and fused, and compare with the oracle; the launch must report the
+    forced variant."""
+    if geom == "horizontal":  # every band row starts on a pair: the EVEN kernel is eligible
+        aw, ah, nh, nv, bl, W, H, dmax = 4, 1, 2, 0, 1.0, 150, 40, 39
+    else:  # vertical neighbours with fractional shifts: odd band-row starts.  Few levels, so
+        # that even the 32-level chunk's band at 256 columns fits the 160 KB LDS
+        aw, ah, nh, nv, bl, W, H, dmax = 2, 3, 1, 1, 1.0359, 120, 56, 4
+    stack, _ = synth.make_stack(W, H, aw, ah, 0, dmax, bl, 77 + K)
+    cam = _array(aw, ah, 0, dmax, nh=nh, nv=nv, bl=bl)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    l8h = l8.cpu().numpy()
+    box = eng.box_stats(l8, K)
+    z = 1 if geom == "horizontal" else 3
+    want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, bl, K, z)
+    od, oc = orc.wta(want, cam.levels)
+    evens = set()
+    for nw, dpw in _VARIANTS:
+        for bw in (128, 192, 256):
+            for general in (False, True):
+                eng.set_ncc_variant(nw, dpw, bw, general)
+                tag = f"K{K} nw{nw} dpw{dpw} bw{bw} general{int(general)}"
+                vol = eng.ncc_volume(l8, box, cam, z, K)
+                v = eng.ncc_last_variant()
+                assert (v["K"], v["NW"], v["DPW"], v["BW"], v["FUSE"]) == (K, nw, dpw, bw, 0), (tag, v)
+                if general:
+                    assert v["EVEN"] == 0, (tag, v)
+                evens.add(v["EVEN"])
+                same(vol, want, f"volume {tag}")
+                fd, fc = eng.ncc_wta(l8, box, cam, z, K)
+                v = eng.ncc_last_variant()
+                assert (v["NW"], v["DPW"], v["BW"], v["FUSE"]) == (nw, dpw, bw, 1), (tag, v)
+                same(fd, od, f"fused disp {tag}")
+                same(fc, oc, f"fused conf {tag}")
+    # K = 5 horizontal bands start on a row pair (R + tymax even); K = 7 (R = 3)
+    # and fractional vertical shifts start on odd rows
+    assert evens == ({0, 1} if geom == "horizontal" and K == 5 else {0})

@@ -64,10 +64,48 @@ def test_view_ranges_tile_the_full_result(engine, world):
         engine.propagate(full, lb, rep, flat, cam, S, 0, rp["prop_alpha"], rp["prop_gamma"], rp["fuse"], nks, kss,
                          st, bpart, z0, z1)
     assert torch.equal(a, bpart)
+    ipart = torch.full_like(st, float("nan"))
+    for z0, z1 in all_blocks(V, world):
+        engine.init_state_range(full, lb, rep, flat, cam, S, rp["init_gamma"], rp["init_alpha"], rp["kernel_steps"],
+                                rp["kss"], rp["fuse"], z0, z1, state=ipart)
+    assert torch.equal(st, ipart)
     disp = engine.spixl_to_image(full, lb, a, S)
-    _, f_full = engine.filter(disp, c["aw"], c["bl"], 1.0)
+    p_full, f_full = engine.filter(disp, c["aw"], c["bl"], 1.0)
     f_part = torch.zeros_like(f_full)
+    p_part = torch.full_like(p_full, float("nan"))
     for z0, z1 in all_blocks(V, world):
         _, o = engine.filter(disp, c["aw"], c["bl"], 1.0, z0, z1)
         f_part[z0:z1] = o[z0:z1]
+        engine.proj_inv(disp, c["aw"], c["bl"], z0, z1, proj=p_part)
+    assert torch.equal(p_full, p_part)
+    r_part = torch.zeros_like(f_full)
+    for z0, z1 in all_blocks(V, world):
+        engine.remove_inconsistency(disp, p_part, c["aw"], c["bl"], 1.0, z0, z1, out=r_part)
     assert torch.equal(f_full, f_part)
+    assert torch.equal(f_full, r_part)
+
+
+def test_view_subsets_of_cvt_and_window_planes(engine):
+    """cvt / window planes restricted to a shard's views equal the full ones on
+    those views (and leave the others untouched)."""
+    c = dict(CASES["c3x3_s8"])
+    b = build(c)
+    rgbx = torch.from_numpy(b["stack"]).cuda()
+    lab, l8 = engine.cvt(rgbx)
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
+    views = cam.views_needed(0, 2)
+    assert views == sorted(set([0, 1] + list(b["vs"][0, :b["sn"][0]]) + list(b["vs"][1, :b["sn"][1]])))
+    lab2 = torch.full_like(lab, float("nan"))
+    l82 = torch.zeros_like(l8)
+    engine.cvt_views(rgbx, views, lab2, l82)
+    for v in range(b["V"]):
+        if v in views:
+            assert torch.equal(lab2[v], lab[v]) and torch.equal(l82[v], l8[v])
+        else:
+            assert torch.isnan(lab2[v]).all()
+    for K in (5, 7):
+        box = engine.box_stats(l8, K)
+        box2 = torch.zeros_like(box)
+        engine.box_stats_views(l8, K, views, box2)
+        for v in views:
+            assert torch.equal(box[:, v], box2[:, v])

@@ -273,8 +273,8 @@ int mvs_sweep_pixel_sad_d(mvs_ctx* c, int W, int H, const float* lab, const mvs_
   if (!c || !lab || !disp || bad_dims(W, H)) return mvs::arg_fail("mvs_sweep_pixel_sad_d: bad arguments");
   RC(upload_meta(c, a));
   if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_sweep_pixel_sad_d: bad view range");
-  return mvs::launch_sweep_pixel_sad(c->stream, a->view_count, W, H, lab, c->d_levels, a->num_levels, c->d_vs,
-                                     c->d_sn, a->subset_num, a->array_width, a->bl_ratio, z0, z1, disp);
+  return mvs::launch_sweep_pixel_sad(c, a->view_count, W, H, lab, a->levels, a->num_levels, a->view_subset,
+                                     a->subset_num, a->array_width, a->bl_ratio, z0, z1, disp);
 }
 
 int mvs_box_stats_d(mvs_ctx* c, const uint8_t* l8, int V, int W, int H, int K, int32_t* box) {

@@ -81,9 +81,8 @@ int launch_boundary(hipStream_t s, int V, int W, int H, int S, const float* spix
 int launch_sweep_spixl(hipStream_t s, int V, int W, int H, int S, const float* lab, float* spixl,
                        const uint8_t* rep, const float* levels, int D, const int* vs, const int* sn, int aw,
                        float bl, int z0, int z1);
-int launch_sweep_pixel_sad(hipStream_t s, int V, int W, int H, const float* lab, const float* levels, int D,
-                           const int* vs, const int* sn, const int* sn_host, int aw, float bl, int z0, int z1,
-                           float* disp);
+int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
+                           const int* vs_host, const int* sn_host, int aw, float bl, int z0, int z1, float* disp);
 int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int K, int32_t* box, int z0, int z1);
 int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
                       const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol,

@@ -4,16 +4,24 @@
 //  k_sweep_spixl     initial_depth_estimation_v2          clcode.cl:972-1069
 //                    (one wave per superpixel, lanes over hypotheses,
 //                    exact first-minimum WTA by a (cost, index) wave reduction)
-//  k_sweep_pixel_sad the same sweep at S=1 grid semantics (reference-parity
-//                    per-pixel mode): 32x32 output tile per workgroup, the
-//                    per-tap absolute differences of one (d, neighbour) staged
-//                    in LDS as (c, a) pairs so the reference's
-//                    val+=30 / val-=30 / val+=AD sequence is three branch-free
-//                    adds per tap, summed in the reference's window order.
+//  k_sad_band        the same sweep at S=1 grid semantics (reference-parity
+//                    per-pixel mode): per (chunk of levels, neighbour) the
+//                    neighbour's Lab band is staged in LDS once (LDS-DMA,
+//                    double-buffered) and serves every level of the chunk; per
+//                    level pair a wave stages the taps' absolute differences
+//                    in LDS and sums each pixel's 25 taps in the reference's
+//                    order as v_pk_add_f32 over the two levels.
+//  k_sweep_pixel_sad the first per-pixel form (every (d, neighbour) region
+//                    gathered from global memory): kept for level sets with
+//                    fractional column shifts.
 //  (the NCC cost-volume kernels are in ncc.hip)
 //  k_wta             winner-take-all + confidence over the materialised volume
 //                    (the HBM-streaming pass the roofline is quoted on).
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "mvs_internal.h"
 
@@ -176,6 +184,274 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       }
     }
     spixl[8 * idx + 7] = (bi != 0x7fffffff && best < 1000000.0f) ? levels[bi] : 0.0f;
+  }
+}
+
+// ---- per-pixel SAD sweep on LDS bands (S=1 grid semantics) -----------------
+// Tile: 60 output columns x TH rows; its 64 x (TH+4) tap region (2-pixel
+// halo) has one region column per lane.  Steps t = (chunk c of DC = 8*PPW
+// levels, neighbour n): the neighbour's Lab rows and columns reachable from
+// the region at any level of the chunk are staged in LDS once per step and
+// serve every level of the chunk.  The next step's band is loaded into
+// registers at the start of a step and written to the other LDS buffer after
+// the step's compute, so its latency hides behind the compute.  Wave w takes
+// the chunk's level pairs w*PPW .. w*PPW+PPW-1; per pair:
+//   A. each lane forms its region column's taps a = |dL|+|da|+|db| of both
+//      levels from its reference colours (registers) and the band, or 30 for
+//      a tap outside the image (ref or projection), into a wave-private LDS
+//      plane of float2 {level 2p, level 2p+1};
+//   B. each lane sums its output pixel's 25 taps, x offset outer and y offset
+//      inner as the reference does, val = ((val + 30) - 30) + a, as three
+//      v_pk_add_f32 over the pair.  (An out-of-image tap with a = 30 gives
+//      RN(RN(RN(val+30) - 30) + 30) = RN(val+30): RN(val+30) - 30 is exact for
+//      val >= 0, so this is the reference's lone val += 30, bit for bit.)
+// The per-level minimum over neighbours folds into a first-minimum WTA in
+// level order; the 4 waves' (cost, level) winners are merged
+// lexicographically at the end.
+constexpr int SB_TW = 60;   // output columns per tile
+constexpr int SB_ADW = 68;  // AD plane pitch (float2): lanes 60..63 read up to column 67
+constexpr int SB_RPW = 6;   // band rows per wave the prefetch holds (band rows <= 24)
+constexpr int SB_NBLK = 2;  // 64-column blocks per band row (band columns <= 128)
+constexpr float SB_INIT = 1000000.0f;
+
+struct SadArgs {
+  int W, H, D, nn, z;
+  int tiles_x, ntiles, tiles_per_xcd, nch;
+  int bw, brows;  // LDS band pitch (pixels) and rows per buffer
+};
+// host-built plan, one record per step (c, n), read by scalar loads
+struct alignas(16) SadRec {
+  int view, sxmin, sxmax, pad0;
+  float fdymin, fdymax;
+  int pad1[2];
+  int sx[16];     // per level j of the chunk: column shift d*dx (integral)
+  float fdy[16];  // per level j: (bl*d)*dy, the reference's float row shift
+};
+
+// the band of step record e for the tile at (x0, y0): every neighbour pixel a
+// valid tap of the region can project to at any level of the chunk
+struct SadBand {
+  int bx0, by0, nrows, ncols;
+};
+template <int TH>
+__device__ __forceinline__ SadBand sad_band_of(const SadRec& e, int x0, int y0, int W, int H) {
+  SadBand g;
+  g.bx0 = min(max(x0 - 2 - e.sxmax, 0), W - 1);
+  const int bx1 = min(max(x0 + SB_TW + 1 - e.sxmin, 0), W - 1);
+  g.by0 = min(max((int)((float)(y0 - 2) - e.fdymax), 0), H - 1);
+  const int by1 = min(max((int)((float)(y0 + TH + 1) - e.fdymin), 0), H - 1);
+  g.nrows = by1 - g.by0 + 1;
+  g.ncols = bx1 - g.bx0 + 1;
+  return g;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// MODE 0: register-staged band prefetch (default); 1: load + store the band at
+// the start of its own step (no overlap; A/B reference)
+template <int TH, int PPW, int MODE>
+__global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab, const float* __restrict__ levels,
+                                                  const SadRec* __restrict__ plan, SadArgs a,
+                                                  float* __restrict__ disp) {
+  constexpr int RR = TH + 4, DC = 8 * PPW;
+  extern __shared__ __align__(16) uint8_t smem[];
+  float4* band = (float4*)smem;                                 // [2][brows][bw]
+  float2* adb = (float2*)(band + 2 * a.brows * a.bw);           // [4 waves][RR][SB_ADW]
+  int* rtab = (int*)(adb + 4 * RR * SB_ADW);                    // [2][DC][RR]
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware tile map (as k_ncc_volume): each XCD a contiguous strip of tiles
+  const int bid = blockIdx.x, grp = bid & 7;
+  const int tile = grp * a.tiles_per_xcd + (bid >> 3);
+  if (tile >= a.ntiles) return;
+  const int W = a.W, H = a.H;
+  const int x0 = (tile % a.tiles_x) * SB_TW, y0 = (tile / a.tiles_x) * TH;
+  const long P = (long)W * H;
+  const int gx = x0 - 2 + lane;  // this lane's region column
+  const bool gxok = gx >= 0 && gx < W;
+  float rL[RR], ra[RR], rb[RR];
+  {
+    const float4* labz = lab + (long)a.z * P;
+#pragma unroll
+    for (int r = 0; r < RR; r++) {
+      const int gy = y0 - 2 + r;
+      const bool in = gxok && gy >= 0 && gy < H;
+      const float4 c = labz[in ? (long)gy * W + gx : 0];
+      rL[r] = c.x;
+      ra[r] = c.y;
+      rb[r] = c.z;
+    }
+  }
+  float2* myad = adb + wave * RR * SB_ADW;
+  const int T = a.nch * a.nn;
+
+  float4 pf[SB_RPW][SB_NBLK];
+  SadBand pg{0, 0, 0, 0};
+  // global -> registers: step t's band, wave w holding rows w, w+4, ...
+  auto fetch = [&](int t) {
+    const SadRec& e = plan[t];
+    pg = sad_band_of<TH>(e, x0, y0, W, H);
+    const float4* src = lab + (long)e.view * P + (long)pg.by0 * W + pg.bx0;
+#pragma unroll
+    for (int m = 0; m < SB_RPW; m++)
+#pragma unroll
+      for (int cb = 0; cb < SB_NBLK; cb++) {
+        const int i = wave + 4 * m, col = cb * 64 + lane;
+        if (i < pg.nrows && col < pg.ncols) pf[m][cb] = src[(long)i * W + col];
+      }
+  };
+  // registers -> LDS buffer b, and step t's row table: per (level j, region
+  // row r) the band index of row yp minus bx0 (so + xp gives the pixel), or -1
+  // when the reference row or the projected row leaves the image
+  auto commit = [&](int t, int b) {
+    const SadRec& e = plan[t];
+    float4* dst = band + b * a.brows * a.bw;
+#pragma unroll
+    for (int m = 0; m < SB_RPW; m++)
+#pragma unroll
+      for (int cb = 0; cb < SB_NBLK; cb++) {
+        const int i = wave + 4 * m, col = cb * 64 + lane;
+        if (i < pg.nrows && col < pg.ncols) dst[i * a.bw + col] = pf[m][cb];
+      }
+    int* tb = rtab + b * DC * RR;
+    const int c = t / a.nn;
+    for (int k = tid; k < DC * RR; k += 256) {
+      const int j = k / RR, r = k - j * RR;
+      const int gy = y0 - 2 + r;
+      int v = -1;
+      if (c * DC + j < a.D) {
+        const int yp = (int)((float)gy - e.fdy[j]);
+        if (gy >= 0 && gy < H && yp >= 0 && yp < H) v = (yp - pg.by0) * a.bw - pg.bx0;
+      }
+      tb[k] = v;
+    }
+  };
+
+  float best[TH];
+  int bidx[TH];
+#pragma unroll
+  for (int o = 0; o < TH; o++) {
+    best[o] = SB_INIT;
+    bidx[o] = -1;
+  }
+  f32x2 mn[PPW][TH];
+  if (T > 0) {
+    fetch(0);
+    commit(0, 0);
+  }
+  __syncthreads();
+  for (int t = 0; t < T; t++) {
+    if (MODE == 1 && t > 0) {
+      fetch(t);
+      commit(t, t & 1);
+      __syncthreads();
+    }
+    if (MODE == 0 && t + 1 < T) fetch(t + 1);  // lands in registers while this step computes
+    const int c = t / a.nn, n = t - c * a.nn;
+    if (n == 0) {
+#pragma unroll
+      for (int q = 0; q < PPW; q++)
+#pragma unroll
+        for (int o = 0; o < TH; o++) mn[q][o] = f32x2{SB_INIT, SB_INIT};
+    }
+    const SadRec& e = plan[t];
+    const float4* bnd = band + (t & 1) * a.brows * a.bw;
+    const int* tb = rtab + (t & 1) * DC * RR;
+#pragma unroll
+    for (int q = 0; q < PPW; q++) {
+      const int j0 = (wave * PPW + q) * 2;
+      const int xp0 = gx - e.sx[j0], xp1 = gx - e.sx[j0 + 1];
+      const bool xok0 = gxok && xp0 >= 0 && xp0 < W, xok1 = gxok && xp1 >= 0 && xp1 < W;
+      // A. taps of the lane's region column, both levels
+#pragma unroll
+      for (int r = 0; r < RR; r++) {
+        const int t0 = tb[j0 * RR + r], t1 = tb[(j0 + 1) * RR + r];
+        const bool v0 = xok0 && t0 >= 0, v1 = xok1 && t1 >= 0;
+        const float4 n0 = bnd[v0 ? t0 + xp0 : 0], n1 = bnd[v1 ? t1 + xp1 : 0];
+        asm volatile("" ::"v"(n0.w), "v"(n1.w));  // keep the full 16-B ds_read_b128 (b96 is 3x slower)
+        float d0 = fabsf(rL[r] - n0.x) + fabsf(ra[r] - n0.y);
+        d0 = d0 + fabsf(rb[r] - n0.z);
+        float d1 = fabsf(rL[r] - n1.x) + fabsf(ra[r] - n1.y);
+        d1 = d1 + fabsf(rb[r] - n1.z);
+        myad[r * SB_ADW + lane] = make_float2(v0 ? d0 : 30.0f, v1 ? d1 : 30.0f);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // B. 25-tap sums: x offset outer, y offset inner (clcode.cl:1017-1047
+      // order per output); the TH outputs' chains interleave
+      f32x2 acc[TH];
+#pragma unroll
+      for (int o = 0; o < TH; o++) acc[o] = f32x2{0.0f, 0.0f};
+      const f32x2 k30 = f32x2{30.0f, 30.0f};
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        f32x2 col[RR];
+#pragma unroll
+        for (int r = 0; r < RR; r++) {
+          const float2 v = myad[r * SB_ADW + lane + i];
+          col[r] = f32x2{v.x, v.y};
+        }
+#pragma unroll
+        for (int jj = 0; jj < 5; jj++)
+#pragma unroll
+          for (int o = 0; o < TH; o++) acc[o] = ((acc[o] + k30) - k30) + col[o + jj];
+      }
+#pragma unroll
+      for (int o = 0; o < TH; o++) {
+        mn[q][o].x = fminf(mn[q][o].x, acc[o].x);
+        mn[q][o].y = fminf(mn[q][o].y, acc[o].y);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (n == a.nn - 1) {  // chunk complete: first-minimum WTA in level order
+#pragma unroll
+      for (int q = 0; q < PPW; q++) {
+        const int dl = c * DC + (wave * PPW + q) * 2;
+#pragma unroll
+        for (int o = 0; o < TH; o++) {
+          if (dl < a.D && mn[q][o].x < best[o]) {
+            best[o] = mn[q][o].x;
+            bidx[o] = dl;
+          }
+          if (dl + 1 < a.D && mn[q][o].y < best[o]) {
+            best[o] = mn[q][o].y;
+            bidx[o] = dl + 1;
+          }
+        }
+      }
+    }
+    // the prefetched band into the other buffer (last read in step t-1, before
+    // the previous barrier), then publish it
+    if (MODE == 0 && t + 1 < T) commit(t + 1, (t + 1) & 1);
+    __syncthreads();
+  }
+  // merge the 4 waves' winners: lexicographic (cost, level)
+  float* mb = (float*)smem;
+  int* mi = (int*)(mb + 4 * TH * 64);
+#pragma unroll
+  for (int o = 0; o < TH; o++) {
+    mb[(wave * TH + o) * 64 + lane] = best[o];
+    mi[(wave * TH + o) * 64 + lane] = bidx[o];
+  }
+  __syncthreads();
+  for (int k = tid; k < TH * 64; k += 256) {
+    const int o = k >> 6, l = k & 63;
+    const int x = x0 + l, y = y0 + o;
+    if (l >= SB_TW || x >= W || y >= H) continue;
+    float bv = mb[k];
+    int bi = mi[k];
+#pragma unroll
+    for (int w = 1; w < 4; w++) {
+      const float v = mb[w * TH * 64 + k];
+      const int i = mi[w * TH * 64 + k];
+      if (i >= 0 && (v < bv || (v == bv && (bi < 0 || i < bi)))) {
+        bv = v;
+        bi = i;
+      }
+    }
+    disp[(long)y * W + x] = (bi >= 0 && bv < SB_INIT) ? levels[bi] : 0.0f;
   }
 }
 
@@ -367,16 +643,100 @@ int launch_sweep_spixl(hipStream_t s, int V, int W, int H, int S, const float* l
   return 0;
 }
 
-int launch_sweep_pixel_sad(hipStream_t s, int V, int W, int H, const float* lab, const float* levels, int D,
-                           const int* vs, const int* sn, const int* sn_host, int aw, float bl, int z0, int z1,
-                           float* disp) {
-  (void)sn_host;
-  long P = (long)W * H;
+namespace {
+// Band-staged SAD sweep: host plan + launch for one reference view.  Returns 1
+// when the level set has fractional column shifts or the bands do not fit
+// the LDS (the caller then uses k_sweep_pixel_sad).
+template <int TH, int PPW, int MODE = 0>
+int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
+                      const int* vs_host, const int* sn_host, int aw, float bl, int z, float* disp) {
+  constexpr int RR = TH + 4, DC = 8 * PPW;
+  const int nn = sn_host[z];
+  const int nch = (D + DC - 1) / DC;
+  const int rx = z % aw, ry = z / aw;
+  constexpr int RW = sizeof(SadRec) / 4;
+  std::vector<int32_t> table((size_t)std::max(1, nch * nn) * RW, 0);
+  int span_x = 0;
+  float span_y = 0.0f;
+  for (int c = 0; c < nch; c++)
+    for (int n = 0; n < nn; n++) {
+      SadRec e{};
+      const int view = vs_host[V * z + n];
+      const int dx = view % aw - rx, dy = view / aw - ry;
+      e.view = view;
+      e.sxmin = 1 << 30;
+      e.sxmax = -(1 << 30);
+      e.fdymin = INFINITY;
+      e.fdymax = -INFINITY;
+      for (int j = 0; j < DC; j++) {
+        const int dl = std::min(c * DC + j, D - 1);  // past the end: the last level (rows masked)
+        const float d = levels_host[dl];
+        const float fdx = d * (float)dx;  // the reference's float shifts (clcode.cl:1033-1034)
+        const float fdy = (bl * d) * (float)dy;
+        if (fdx != std::trunc(fdx) || std::fabs(fdx) > 1e6f) return 1;
+        e.sx[j] = (int)fdx;
+        e.fdy[j] = fdy;
+        if (c * DC + j < D) {
+          e.sxmin = std::min(e.sxmin, e.sx[j]);
+          e.sxmax = std::max(e.sxmax, e.sx[j]);
+          e.fdymin = std::min(e.fdymin, fdy);
+          e.fdymax = std::max(e.fdymax, fdy);
+        }
+      }
+      span_x = std::max(span_x, e.sxmax - e.sxmin);
+      span_y = std::max(span_y, e.fdymax - e.fdymin);
+      std::memcpy(table.data() + ((size_t)c * nn + n) * RW, &e, sizeof(SadRec));
+    }
+  SadArgs a{};
+  a.W = W; a.H = H; a.D = D; a.nn = nn; a.z = z; a.nch = nch;
+  a.bw = 64 + span_x;
+  a.brows = RR + (int)std::ceil(span_y) + 2;
+  const size_t lds = 16 * 2 * (size_t)a.brows * a.bw + 8 * 4 * (size_t)RR * SB_ADW + 4 * 2 * (size_t)DC * RR;
+  // the prefetch holds at most 4 * SB_RPW band rows of SB_NBLK * 64 columns
+  if (a.brows > 4 * SB_RPW || a.bw > 64 * SB_NBLK) return 1;
+  if (lds > 160 * 1024 || (size_t)4 * TH * 64 * 8 > 16 * 2 * (size_t)a.brows * a.bw) return 1;
+  int rc = 0;
+  const int32_t* dev = plan_upload(ctx, table, &rc);
+  if (rc) return rc;
+  a.tiles_x = (W + SB_TW - 1) / SB_TW;
+  a.ntiles = a.tiles_x * ((H + TH - 1) / TH);
+  a.tiles_per_xcd = (a.ntiles + 7) / 8;
+  auto kern = k_sad_band<TH, PPW, MODE>;
+  if (lds > 64 * 1024)
+    MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            "hipFuncSetAttribute(sad lds)");
+  hipLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(256), lds, ctx->stream, (const float4*)lab,
+                     ctx->d_levels, (const SadRec*)dev, a, disp);
+  MVS_LAUNCH_CHECK("k_sad_band");
+  return 0;
+}
+
+}  // namespace
+
+int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
+                           const int* vs_host, const int* sn_host, int aw, float bl, int z0, int z1, float* disp) {
+  // MVS_SAD_KERNEL: "band8" (default), "band8x2", "band16", "gather" (A/B)
+  const char* kv = getenv("MVS_SAD_KERNEL");
+  const std::string kind = kv ? kv : "band8";
+  const long P = (long)W * H;
   for (int z = z0; z < z1; z++) {
-    SweepArgs a{V, W, H, W, H, D, aw, z, bl};
-    hipLaunchKernelGGL(k_sweep_pixel_sad, dim3((W + PT - 1) / PT, (H + PT - 1) / PT), dim3(256), 0, s,
-                       (const float4*)lab, levels, vs, sn, a, disp + (long)(z - z0) * P);
-    MVS_LAUNCH_CHECK("k_sweep_pixel_sad");
+    float* out = disp + (long)(z - z0) * P;
+    int rc = 1;
+    if (kind == "band8")
+      rc = launch_sad_band_t<8, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    else if (kind == "band8x2")
+      rc = launch_sad_band_t<8, 2>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    else if (kind == "band8s")
+      rc = launch_sad_band_t<8, 1, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    else if (kind == "band16")
+      rc = launch_sad_band_t<16, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    if (rc < 0) return rc;
+    if (rc == 1) {
+      SweepArgs a{V, W, H, W, H, D, aw, z, bl};
+      hipLaunchKernelGGL(k_sweep_pixel_sad, dim3((W + PT - 1) / PT, (H + PT - 1) / PT), dim3(256), 0, ctx->stream,
+                         (const float4*)lab, ctx->d_levels, ctx->d_vs, ctx->d_sn, a, out);
+      MVS_LAUNCH_CHECK("k_sweep_pixel_sad");
+    }
   }
   return 0;
 }

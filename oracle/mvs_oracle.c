@@ -22,7 +22,18 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* MVS_CONTRACT_PROBE (oracle/Makefile `contract`): the same restatement built
+ * by clang with -ffp-contract=on -mfma, i.e. the reference build's OpenCL
+ * default (mul+add fused inside one expression), to measure how far the
+ * pinned no-contraction definition sits from a contracting build.  The pinned
+ * builtins (mvs_detmath.h) stay uncontracted in both. */
+#ifdef MVS_CONTRACT_PROBE
+#pragma clang fp contract(off)
+#endif
 #include "../include/mvs_detmath.h"
+#ifdef MVS_CONTRACT_PROBE
+#pragma clang fp contract(on)
+#endif
 
 #define LOCAL 16 /* LOCAL_SIZE_UPDATE, header.h:37-38 */
 

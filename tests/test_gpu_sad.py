@@ -1,0 +1,83 @@
+"""GPU parity of the per-pixel SAD sweep (initial_depth_estimation_v2 at S=1
+grid semantics, clcode.cl:972-1069: the reference's own cost) against the
+oracle (orc_sweep_pixel_sad), at the BASELINE configurations' geometry and on
+the edge cases of the band-staged kernel (k_sad_band): image borders, ragged
+tiles, levels past the last chunk, vertical neighbours with fractional row
+shifts (bl_ratio 1.0359), no neighbours, textureless ties.  Bar: bit-exact."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cl_multiview_stereo_amd import params, synth
+from cl_multiview_stereo_amd.engine import CameraArray
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _cam(aw, ah, dmin, dmax, nh, nv, bl, inc=1):
+    vs, sn = params.flatten_subsets(params.neighbour_lists(aw, ah, nh, nv))
+    return CameraArray(aw, bl, params.disparity_levels(dmin, dmax, inc), vs, sn)
+
+
+def _check(engine, stack, cam, z0=0, z1=None, tag=""):
+    lab, _ = engine.cvt(torch.from_numpy(stack).cuda())
+    V = stack.shape[0]
+    z1 = V if z1 is None else z1
+    got = engine.sweep_pixel_sad(lab, cam, z0, z1).cpu().numpy()
+    want = orc.sweep_pixel_sad(lab.cpu().numpy(), cam.levels, cam.view_subset, cam.subset_num, cam.array_width,
+                               cam.bl_ratio, z0, z1)
+    bad = np.count_nonzero(got.view(np.uint32) != want.view(np.uint32))
+    assert bad == 0, f"{tag}: {bad}/{got.size} disparities differ, first {np.argwhere(got != want)[:3].tolist()}"
+
+
+@pytest.mark.parametrize("z", [0, 2])
+def test_sad_c2_band(engine, z):
+    """C2's array (5x1, 4 neighbours up to 4 views away, levels 0..127) on a
+    full-width 1080p band of 40 rows."""
+    stack, _ = synth.make_stack(1920, 40, 5, 1, 0, 127, 1.0, 0x5EED + 2)
+    _check(engine, stack, _cam(5, 1, 0, 127, 4, 0, 1.0), z, z + 1, f"c2 band z{z}")
+
+
+def test_sad_reference_defaults_geometry(engine):
+    """The reference's own 3x3 array with bl_ratio 1.0359 (fractional vertical
+    shifts, per-row truncation), levels 30..60, every view."""
+    stack, _ = synth.make_stack(200, 70, 3, 3, 30, 60, 1.0359, 99)
+    _check(engine, stack, _cam(3, 3, 30, 60, 1, 1, 1.0359), tag="3x3")
+
+
+@pytest.mark.parametrize("W,H,D", [(61, 9, 1), (60, 8, 7), (121, 17, 9), (37, 29, 13), (250, 33, 40)])
+def test_sad_ragged(engine, W, H, D):
+    """Tile edges (60 x 8 tiles), level counts around the 8-level chunk."""
+    stack, _ = synth.make_stack(W, H, 3, 1, 0, D - 1, 1.0, W * 7 + H)
+    _check(engine, stack, _cam(3, 1, 0, D - 1, 2, 0, 1.0), tag=f"{W}x{H} D{D}")
+
+
+def test_sad_level_step_and_offset(engine):
+    stack, _ = synth.make_stack(130, 40, 4, 2, 3, 45, 1.0359, 5)
+    _check(engine, stack, _cam(4, 2, 3, 45, 2, 1, 1.0359, inc=3), tag="inc3")
+
+
+def test_sad_ties_and_no_neighbours(engine):
+    """Flat patches (equal costs at many levels: the first minimum in level
+    order must win across the waves' level subsets) and a view whose
+    neighbour list is empty (disparity 0 everywhere)."""
+    stack, _ = synth.make_stack(150, 40, 3, 1, 0, 23, 1.0, 8)
+    stack[:, 5:30, 20:90, :3] = 90
+    cam = _cam(3, 1, 0, 23, 1, 0, 1.0)
+    cam.subset_num[0] = 0
+    cam = CameraArray(cam.array_width, cam.bl_ratio, cam.levels, cam.view_subset, cam.subset_num)
+    _check(engine, stack, cam, tag="ties")
+
+
+@pytest.mark.parametrize("kind", ["band8", "band8x2", "band16", "band8s", "gather"])
+def test_sad_kernel_variants(engine, kind, monkeypatch):
+    """Every instantiation (MVS_SAD_KERNEL is read per call) on a 3x3 array."""
+    monkeypatch.setenv("MVS_SAD_KERNEL", kind)
+    stack, _ = synth.make_stack(140, 50, 3, 3, 0, 20, 1.0359, 12)
+    _check(engine, stack, _cam(3, 3, 0, 20, 1, 1, 1.0359), tag=kind)
+    assert os.environ["MVS_SAD_KERNEL"] == kind

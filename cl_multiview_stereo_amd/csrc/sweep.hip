@@ -213,6 +213,9 @@ constexpr int SB_ADW = 68;  // AD plane pitch (float2): lanes 60..63 read up to 
 constexpr int SB_RPW = 6;   // band rows per wave the prefetch holds (band rows <= 24)
 constexpr int SB_NBLK = 2;  // 64-column blocks per band row (band columns <= 128)
 constexpr float SB_INIT = 1000000.0f;
+// row-table entry of a row outside the image: a valid entry (yp-by0)*bw - bx0
+// is negative on the band's first row whenever bx0 > 0, so no -1 sentinel
+constexpr int SB_NOROW = -0x40000000;
 
 struct SadArgs {
   int W, H, D, nn, z;
@@ -300,8 +303,8 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
       }
   };
   // registers -> LDS buffer b, and step t's row table: per (level j, region
-  // row r) the band index of row yp minus bx0 (so + xp gives the pixel), or -1
-  // when the reference row or the projected row leaves the image
+  // row r) the band index of row yp minus bx0 (so + xp gives the pixel), or
+  // SB_NOROW when the reference row or the projected row leaves the image
   auto commit = [&](int t, int b) {
     const SadRec& e = plan[t];
     float4* dst = band + b * a.brows * a.bw;
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
     for (int k = tid; k < DC * RR; k += 256) {
       const int j = k / RR, r = k - j * RR;
       const int gy = y0 - 2 + r;
-      int v = -1;
+      int v = SB_NOROW;
       if (c * DC + j < a.D) {
         const int yp = (int)((float)gy - e.fdy[j]);
         if (gy >= 0 && gy < H && yp >= 0 && yp < H) v = (yp - pg.by0) * a.bw - pg.bx0;
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
 #pragma unroll
       for (int r = 0; r < RR; r++) {
         const int t0 = tb[j0 * RR + r], t1 = tb[(j0 + 1) * RR + r];
-        const bool v0 = xok0 && t0 >= 0, v1 = xok1 && t1 >= 0;
+        const bool v0 = xok0 && t0 != SB_NOROW, v1 = xok1 && t1 != SB_NOROW;
         const float4 n0 = bnd[v0 ? t0 + xp0 : 0], n1 = bnd[v1 ? t1 + xp1 : 0];
         asm volatile("" ::"v"(n0.w), "v"(n1.w));  // keep the full 16-B ds_read_b128 (b96 is 3x slower)
         float d0 = fabsf(rL[r] - n0.x) + fabsf(ra[r] - n0.y);
@@ -715,9 +718,13 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
 
 int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
                            const int* vs_host, const int* sn_host, int aw, float bl, int z0, int z1, float* disp) {
-  // MVS_SAD_KERNEL: "band8" (default), "band8x2", "band16", "gather" (A/B)
+  // MVS_SAD_KERNEL: "band8" (default), "band8x2", "band16", "band8s", "gather"
+  // (A/B and tests).  Without it, a geometry the band kernel cannot stage falls
+  // back to the gather kernel; a band variant named explicitly never falls
+  // back (MVS_E_UNSUPPORTED), so a test of it cannot pass on the other kernel.
   const char* kv = getenv("MVS_SAD_KERNEL");
   const std::string kind = kv ? kv : "band8";
+  const bool strict = kv != nullptr && kind != "gather";
   const long P = (long)W * H;
   for (int z = z0; z < z1; z++) {
     float* out = disp + (long)(z - z0) * P;
@@ -731,6 +738,10 @@ int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, 
     else if (kind == "band16")
       rc = launch_sad_band_t<16, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
     if (rc < 0) return rc;
+    if (rc == 1 && strict) {
+      set_error("k_sad_band variant " + kind + " cannot stage this geometry (MVS_SAD_KERNEL set explicitly)");
+      return MVS_E_UNSUPPORTED;
+    }
     if (rc == 1) {
       SweepArgs a{V, W, H, W, H, D, aw, z, bl};
       hipLaunchKernelGGL(k_sweep_pixel_sad, dim3((W + PT - 1) / PT, (H + PT - 1) / PT), dim3(256), 0, ctx->stream,

@@ -14,6 +14,6 @@ for k in ${KINDS:-band8 band8s band8x2 band16 gather}; do
     --no-sharded > gpurun_out/sad/b_$k.json 2> gpurun_out/sad/b_$k.err || exit $?
   python -c "import json;j=json.load(open('gpurun_out/sad/b_$k.json'));print('$k',j['ms_per_step'],j['value'])"
 done
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/sad/trace -o run -- python3 bench.py --config c2 \
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sad/trace -o run -- python3 bench.py --config c2 \
   --cost sad --steps 3 --warmup 1 --no-cpu-baseline --no-sharded > /dev/null 2> gpurun_out/sad/trace.err || exit $?
 f=$(find gpurun_out/sad/trace -name "*kernel_stats.csv" | head -1); head -12 "$f"

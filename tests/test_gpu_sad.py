@@ -74,10 +74,34 @@ def test_sad_ties_and_no_neighbours(engine):
     _check(engine, stack, cam, tag="ties")
 
 
-@pytest.mark.parametrize("kind", ["band8", "band8x2", "band16", "band8s", "gather"])
+# every instantiation on a geometry it can stage: (array, neighbours, bl).  An
+# explicitly named band variant never falls back to the gather kernel
+# (MVS_E_UNSUPPORTED instead), so each case runs the kernel it names.
+_VARIANTS = {
+    "band8": (3, 3, 1, 1, 1.0359),    # vertical shifts: 22 band rows
+    "band8s": (3, 3, 1, 1, 1.0359),
+    "band8x2": (3, 1, 2, 0, 1.0),     # 16-level chunks: horizontal only
+    "band16": (3, 1, 2, 0, 1.0),      # 16-row tiles: horizontal only
+    "gather": (3, 3, 1, 1, 1.0359),
+}
+
+
+@pytest.mark.parametrize("kind", sorted(_VARIANTS))
 def test_sad_kernel_variants(engine, kind, monkeypatch):
-    """Every instantiation (MVS_SAD_KERNEL is read per call) on a 3x3 array."""
+    """Every instantiation (MVS_SAD_KERNEL is read per call), on several tile
+    columns and rows (bx0 > 0 and by0 > 0 bands)."""
     monkeypatch.setenv("MVS_SAD_KERNEL", kind)
-    stack, _ = synth.make_stack(140, 50, 3, 3, 0, 20, 1.0359, 12)
-    _check(engine, stack, _cam(3, 3, 0, 20, 1, 1, 1.0359), tag=kind)
+    aw, ah, nh, nv, bl = _VARIANTS[kind]
+    stack, _ = synth.make_stack(190, 50, aw, ah, 0, 20, bl, 12)
+    _check(engine, stack, _cam(aw, ah, 0, 20, nh, nv, bl), tag=kind)
     assert os.environ["MVS_SAD_KERNEL"] == kind
+
+
+def test_sad_explicit_variant_does_not_fall_back(engine, monkeypatch):
+    """band8x2 cannot stage the 3x3 array's vertical 16-level bands: named
+    explicitly it fails loudly instead of running the gather kernel."""
+    monkeypatch.setenv("MVS_SAD_KERNEL", "band8x2")
+    stack, _ = synth.make_stack(140, 50, 3, 3, 0, 20, 1.0359, 12)
+    lab, _ = engine.cvt(torch.from_numpy(stack).cuda())
+    with pytest.raises(Exception, match="cannot stage"):
+        engine.sweep_pixel_sad(lab, _cam(3, 3, 0, 20, 1, 1, 1.0359), 0, 9)

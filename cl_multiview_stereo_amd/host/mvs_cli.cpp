@@ -82,6 +82,10 @@ int fail(const char* what) {
 // plot_full_image's scaling, clamped
 void to_gray(const float* d, size_t n, int lo, int hi, std::vector<uint8_t>& g) {
   g.resize(n);
+  if (hi == lo) {  // one disparity level: the reference's plot divides by zero; draw a flat map
+    std::fill(g.begin(), g.end(), (uint8_t)0);
+    return;
+  }
   for (size_t i = 0; i < n; i++) {
     float v = std::floor(((d[i] - (float)lo) / (float)(hi - lo)) * 255.0f);
     g[i] = (uint8_t)std::min(255.0f, std::max(0.0f, v));

@@ -11,6 +11,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <fstream>
 #include <iterator>
 
@@ -82,8 +83,20 @@ bool read_png(const std::string& path, Image& img, std::string& err) {
     err = path + ": unsupported PNG (need 8-bit grey/RGB/RGBA, non-interlaced)";
     return false;
   }
+  // the C-ABI's own limit (capi.cpp bad_dims: W*H*16 bytes of Lab < 2^31), checked
+  // before anything is sized from the untrusted header
+  if ((long long)W * H > (1LL << 31) / 16) {
+    err = path + ": image too large (" + std::to_string(W) + "x" + std::to_string(H) + ")";
+    return false;
+  }
   const size_t stride = (size_t)W * ch;
-  std::vector<uint8_t> raw((stride + 1) * H);
+  std::vector<uint8_t> raw;
+  try {
+    raw.resize((stride + 1) * H);
+  } catch (const std::bad_alloc&) {
+    err = path + ": out of host memory";
+    return false;
+  }
   uLongf len = (uLongf)raw.size();
   if (uncompress(raw.data(), &len, z.data(), (uLong)z.size()) != Z_OK || len != raw.size()) {
     err = path + ": corrupt image data";

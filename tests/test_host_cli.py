@@ -67,6 +67,14 @@ def test_errors(cli, tmp_path):
     bad.write_bytes(b"not a png")
     r = subprocess.run([cli, "--png-decode", str(bad), str(tmp_path / "x")], capture_output=True, text=True)
     assert r.returncode == 1 and "not a PNG" in r.stderr
+    # an IHDR asking for 100000 x 100000 pixels is refused before any allocation
+    import struct
+    from pngio import _chunk
+    huge = tmp_path / "huge.png"
+    huge.write_bytes(b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", 100000, 100000, 8, 2, 0, 0, 0))
+                     + _chunk(b"IDAT", b"") + _chunk(b"IEND", b""))
+    r = subprocess.run([cli, "--png-decode", str(huge), str(tmp_path / "x")], capture_output=True, text=True)
+    assert r.returncode == 1 and "too large" in r.stderr
     lst = tmp_path / "one.txt"
     lst.write_text("a.png\n")
     r = subprocess.run([cli, "--data", str(lst), "--array", "2x1"], capture_output=True, text=True)

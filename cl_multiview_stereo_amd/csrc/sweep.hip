@@ -8,9 +8,11 @@
 //                    per-pixel mode): per (chunk of levels, neighbour) the
 //                    neighbour's Lab band is staged in LDS once (LDS-DMA,
 //                    double-buffered) and serves every level of the chunk; per
-//                    level pair a wave stages the taps' absolute differences
-//                    in LDS and sums each pixel's 25 taps in the reference's
-//                    order as v_pk_add_f32 over the two levels.
+//                    level pair a lane forms its column's absolute differences
+//                    and the 25-tap sums run in the reference's order as
+//                    v_pk_add_f32 over the two levels, the window columns
+//                    passed lane to lane by DPP wave_shr (SYS, the default)
+//                    or through an LDS plane (the first, two-phase form).
 //  k_sweep_pixel_sad the first per-pixel form (every (d, neighbour) region
 //                    gathered from global memory): kept for level sets with
 //                    fractional column shifts.
@@ -250,17 +252,30 @@ __device__ __forceinline__ SadBand sad_band_of(const SadRec& e, int x0, int y0, 
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// wave_shr:1 -- lane l receives lane l-1's value (lane 0: 0)
+__device__ __forceinline__ float shr1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+
 // MODE 0: register-staged band prefetch (default); 1: load + store the band at
-// the start of its own step (no overlap; A/B reference)
-template <int TH, int PPW, int MODE>
+// the start of its own step (no overlap; A/B reference).
+// SYS: phase B as a systolic chain across lanes instead of through LDS.  An
+// output's 25-tap chain takes its 5 window columns in order (x offset outer),
+// and window column i of output x is region column x-2+i = lane (x-x0)+i.  So
+// every lane runs the 5-row inner chains of its OWN column's taps (kept in
+// registers) on the partial sums it receives from the lane to its left
+// (DPP wave_shr:1, folded into the first add of each column): after the 5th
+// column, lane l holds the output of image column x0 + l - 4.  The AD plane,
+// its LDS writes/reads and the wave barriers of the two-phase form disappear.
+template <int TH, int PPW, int MODE, bool SYS = false>
 __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab, const float* __restrict__ levels,
                                                   const SadRec* __restrict__ plan, SadArgs a,
                                                   float* __restrict__ disp) {
   constexpr int RR = TH + 4, DC = 8 * PPW;
   extern __shared__ __align__(16) uint8_t smem[];
   float4* band = (float4*)smem;                                 // [2][brows][bw]
-  float2* adb = (float2*)(band + 2 * a.brows * a.bw);           // [4 waves][RR][SB_ADW]
-  int* rtab = (int*)(adb + 4 * RR * SB_ADW);                    // [2][DC][RR]
+  float2* adb = (float2*)(band + 2 * a.brows * a.bw);           // [4 waves][RR][SB_ADW] (two-phase form only)
+  int* rtab = SYS ? (int*)adb : (int*)(adb + 4 * RR * SB_ADW);  // [2][DC][RR]
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware tile map (as k_ncc_volume): each XCD a contiguous strip of tiles
   const int bid = blockIdx.x, grp = bid & 7;
@@ -364,7 +379,9 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
       const int j0 = (wave * PPW + q) * 2;
       const int xp0 = gx - e.sx[j0], xp1 = gx - e.sx[j0 + 1];
       const bool xok0 = gxok && xp0 >= 0 && xp0 < W, xok1 = gxok && xp1 >= 0 && xp1 < W;
+      const f32x2 k30 = f32x2{30.0f, 30.0f};
       // A. taps of the lane's region column, both levels
+      f32x2 ad[RR];
 #pragma unroll
       for (int r = 0; r < RR; r++) {
         const int t0 = tb[j0 * RR + r], t1 = tb[(j0 + 1) * RR + r];
@@ -375,7 +392,35 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
         d0 = d0 + fabsf(rb[r] - n0.z);
         float d1 = fabsf(rL[r] - n1.x) + fabsf(ra[r] - n1.y);
         d1 = d1 + fabsf(rb[r] - n1.z);
-        myad[r * SB_ADW + lane] = make_float2(v0 ? d0 : 30.0f, v1 ? d1 : 30.0f);
+        ad[r] = f32x2{v0 ? d0 : 30.0f, v1 ? d1 : 30.0f};
+        if (!SYS) myad[r * SB_ADW + lane] = make_float2(ad[r].x, ad[r].y);
+      }
+      if (SYS) {
+        // B'. systolic: column 0 starts the chains (first tap: ((0+30)-30)+a = a
+        // exactly), columns 1..4 continue the left neighbour's partials
+        f32x2 p[TH];
+#pragma unroll
+        for (int o = 0; o < TH; o++) {
+          p[o] = ad[o];
+#pragma unroll
+          for (int jj = 1; jj < 5; jj++) p[o] = ((p[o] + k30) - k30) + ad[o + jj];
+        }
+#pragma unroll
+        for (int i = 1; i < 5; i++)
+#pragma unroll
+          for (int o = 0; o < TH; o++) {
+            f32x2 v = f32x2{shr1(p[o].x) + 30.0f, shr1(p[o].y) + 30.0f};
+            v = (v - k30) + ad[o];
+#pragma unroll
+            for (int jj = 1; jj < 5; jj++) v = ((v + k30) - k30) + ad[o + jj];
+            p[o] = v;
+          }
+#pragma unroll
+        for (int o = 0; o < TH; o++) {
+          mn[q][o].x = fminf(mn[q][o].x, p[o].x);
+          mn[q][o].y = fminf(mn[q][o].y, p[o].y);
+        }
+        continue;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -385,7 +430,6 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
       f32x2 acc[TH];
 #pragma unroll
       for (int o = 0; o < TH; o++) acc[o] = f32x2{0.0f, 0.0f};
-      const f32x2 k30 = f32x2{30.0f, 30.0f};
 #pragma unroll
       for (int i = 0; i < 5; i++) {
         f32x2 col[RR];
@@ -441,8 +485,8 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
   __syncthreads();
   for (int k = tid; k < TH * 64; k += 256) {
     const int o = k >> 6, l = k & 63;
-    const int x = x0 + l, y = y0 + o;
-    if (l >= SB_TW || x >= W || y >= H) continue;
+    const int x = SYS ? x0 + l - 4 : x0 + l, y = y0 + o;  // SYS: lane l holds column x0 + l - 4
+    if ((SYS ? l < 4 : l >= SB_TW) || x >= W || y >= H) continue;
     float bv = mb[k];
     int bi = mi[k];
 #pragma unroll
@@ -650,7 +694,7 @@ namespace {
 // Band-staged SAD sweep: host plan + launch for one reference view.  Returns 1
 // when the level set has fractional column shifts or the bands do not fit
 // the LDS (the caller then uses k_sweep_pixel_sad).
-template <int TH, int PPW, int MODE = 0>
+template <int TH, int PPW, int MODE = 0, bool SYS = false>
 int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
                       const int* vs_host, const int* sn_host, int aw, float bl, int z, float* disp) {
   constexpr int RR = TH + 4, DC = 8 * PPW;
@@ -694,7 +738,8 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
   a.W = W; a.H = H; a.D = D; a.nn = nn; a.z = z; a.nch = nch;
   a.bw = 64 + span_x;
   a.brows = RR + (int)std::ceil(span_y) + 2;
-  const size_t lds = 16 * 2 * (size_t)a.brows * a.bw + 8 * 4 * (size_t)RR * SB_ADW + 4 * 2 * (size_t)DC * RR;
+  const size_t lds = 16 * 2 * (size_t)a.brows * a.bw + (SYS ? 0 : 8 * 4 * (size_t)RR * SB_ADW) +
+                     4 * 2 * (size_t)DC * RR;
   // the prefetch holds at most 4 * SB_RPW band rows of SB_NBLK * 64 columns
   if (a.brows > 4 * SB_RPW || a.bw > 64 * SB_NBLK) return 1;
   if (lds > 160 * 1024 || (size_t)4 * TH * 64 * 8 > 16 * 2 * (size_t)a.brows * a.bw) return 1;
@@ -704,7 +749,7 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
   a.tiles_x = (W + SB_TW - 1) / SB_TW;
   a.ntiles = a.tiles_x * ((H + TH - 1) / TH);
   a.tiles_per_xcd = (a.ntiles + 7) / 8;
-  auto kern = k_sad_band<TH, PPW, MODE>;
+  auto kern = k_sad_band<TH, PPW, MODE, SYS>;
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(sad lds)");
@@ -718,18 +763,23 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
 
 int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
                            const int* vs_host, const int* sn_host, int aw, float bl, int z0, int z1, float* disp) {
-  // MVS_SAD_KERNEL: "band8" (default), "band8x2", "band16", "band8s", "gather"
-  // (A/B and tests).  Without it, a geometry the band kernel cannot stage falls
-  // back to the gather kernel; a band variant named explicitly never falls
-  // back (MVS_E_UNSUPPORTED), so a test of it cannot pass on the other kernel.
+  // MVS_SAD_KERNEL: "sys8x2", "sys8", "sys16", "band8", "band8x2", "band16",
+  // "band8s", "gather" (A/B and tests).  Without it: the systolic kernel with
+  // 16-level chunks, else with 8-level chunks (taller bands: vertical
+  // neighbours), else the gather kernel.  A band variant named explicitly never
+  // falls back (MVS_E_UNSUPPORTED), so a test of it cannot pass on another.
   const char* kv = getenv("MVS_SAD_KERNEL");
-  const std::string kind = kv ? kv : "band8";
+  const std::string kind = kv ? kv : "auto";
   const bool strict = kv != nullptr && kind != "gather";
   const long P = (long)W * H;
   for (int z = z0; z < z1; z++) {
     float* out = disp + (long)(z - z0) * P;
     int rc = 1;
-    if (kind == "band8")
+    if (kind == "auto") {
+      rc = launch_sad_band_t<8, 2, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+      if (rc == 1)
+        rc = launch_sad_band_t<8, 1, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    } else if (kind == "band8")
       rc = launch_sad_band_t<8, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
     else if (kind == "band8x2")
       rc = launch_sad_band_t<8, 2>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
@@ -737,6 +787,12 @@ int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, 
       rc = launch_sad_band_t<8, 1, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
     else if (kind == "band16")
       rc = launch_sad_band_t<16, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    else if (kind == "sys8")
+      rc = launch_sad_band_t<8, 1, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    else if (kind == "sys8x2")
+      rc = launch_sad_band_t<8, 2, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    else if (kind == "sys16")
+      rc = launch_sad_band_t<16, 1, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
     if (rc < 0) return rc;
     if (rc == 1 && strict) {
       set_error("k_sad_band variant " + kind + " cannot stage this geometry (MVS_SAD_KERNEL set explicitly)");

@@ -83,6 +83,9 @@ _VARIANTS = {
     "band8x2": (3, 1, 2, 0, 1.0),     # 16-level chunks: horizontal only
     "band16": (3, 1, 2, 0, 1.0),      # 16-row tiles: horizontal only
     "gather": (3, 3, 1, 1, 1.0359),
+    "sys8": (3, 3, 1, 1, 1.0359),     # systolic (DPP) column chain
+    "sys8x2": (3, 1, 2, 0, 1.0),
+    "sys16": (3, 1, 2, 0, 1.0),
 }
 
 

@@ -12,6 +12,8 @@
 // (superpixel, view), candidate plane evaluations in the reference's order.
 // The per-superpixel inputs are packed once per launch into 32-B records so a
 // gather touches one cache line.  Numerics follow include/mvs_detmath.h.
+#include <cstdlib>
+
 #include "mvs_internal.h"
 
 namespace mvs {
@@ -832,7 +834,6 @@ __global__ __launch_bounds__(256) void k_remove_incons_sel(const float* __restri
 // Measured at C4 (32 views): ~86 % of (reference, pixel) pairs have no stable
 // candidate, so every candidate is tried; the selection kernel above repeats
 // the O(V^2) candidate bookkeeping per reference and per try.
-constexpr int FB = 8;  // views per gather block in k_remove_incons_px
 template <int N>
 __device__ __forceinline__ void sort_desc(float (&v)[N]) {
 #pragma unroll
@@ -851,7 +852,7 @@ __device__ __forceinline__ void sort_desc(float (&v)[N]) {
       }
 }
 
-template <int MAXV>
+template <int MAXV, int FB>  // FB: views per gather block (gathers in flight together)
 __global__ __launch_bounds__(256) void k_remove_incons_px(const float* __restrict__ proj, const float* __restrict__ full,
                                                           int V, int W, int H, int aw, float bl, float fuse, int z0,
                                                           int z1, float* __restrict__ out) {
@@ -983,9 +984,25 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
     if (V <= 8)
       hipLaunchKernelGGL(k_remove_incons_sel<8>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
     else if (V <= 16)
-      hipLaunchKernelGGL(k_remove_incons_px<16>, gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1, out);
-    else if (V <= 32)
-      hipLaunchKernelGGL(k_remove_incons_px<32>, gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1, out);
+      hipLaunchKernelGGL((k_remove_incons_px<16, 8>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1,
+                         out);
+    else if (V <= 32) {
+      // MVS_FILTER_FB: views per gather block (A/B; read per call).  Measured at
+      // C4 (scripts/bench_filter.py): blocks of 8 gathers 54 ms for all 32
+      // references, 4: 35 ms, 2: 35 ms -- a candidate's early exit comes after
+      // ~3 gathers, so 8-wide blocks fetched twice what the vote needed
+      const char* fb = getenv("MVS_FILTER_FB");
+      const int nfb = fb ? atoi(fb) : 4;
+      if (nfb == 4)
+        hipLaunchKernelGGL((k_remove_incons_px<32, 4>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0,
+                           z1, out);
+      else if (nfb == 2)
+        hipLaunchKernelGGL((k_remove_incons_px<32, 2>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0,
+                           z1, out);
+      else
+        hipLaunchKernelGGL((k_remove_incons_px<32, 8>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0,
+                           z1, out);
+    }
     else if (V <= 64)
       hipLaunchKernelGGL(k_remove_incons_sel<64>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
     else

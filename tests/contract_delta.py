@@ -10,9 +10,10 @@ the oracle restatement twice on the same synthetic stacks -- the pinned build
 -ffp-contract=on -mfma; the pinned exp/powr stay uncontracted) -- and reports
 per configuration: Lab bits changed, SLIC label flips per view, superpixel
 seed (s7) mismatches, and depth L1 between the two builds' disparity maps.
-CPU only.  Writes profiles/contract_delta.json.
+CPU only (checker infrastructure: it lives under tests/ because it loads the
+oracle).  Writes profiles/contract_delta.json.
 
-    python scripts/contract_delta.py [--configs c1,c2,c3,ref]
+    python tests/contract_delta.py [--configs c1,c2,c3,ref]
 """
 from __future__ import annotations
 

@@ -30,7 +30,7 @@ class MvsError(RuntimeError):
 
 class SlicParams(C.Structure):
     _fields_ = [("spixl_size", C.c_int), ("color_weight", C.c_float), ("no_iter", C.c_int),
-                ("enforce_connectivity", C.c_int)]
+                ("enforce_connectivity", C.c_int), ("edge_enable", C.c_int)]
 
 
 class ArrayDesc(C.Structure):

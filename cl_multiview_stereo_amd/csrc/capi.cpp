@@ -205,13 +205,14 @@ int mvs_grid_d(mvs_ctx* c, const float* lab, int V, int W, int H, int S, float* 
   return mvs::launch_grid_labels(c->stream, V, W, H, S, labels);
 }
 
-int mvs_slic_d(mvs_ctx* c, const float* lab, int V, int W, int H, const mvs_slic_params* p, float* spixl,
+int mvs_slic_d(mvs_ctx* c, float* lab, int V, int W, int H, const mvs_slic_params* p, float* spixl,
                uint32_t* labels) {
   if (!c || !lab || !spixl || !labels || !p || V <= 0 || bad_dims(W, H))
     return mvs::arg_fail("mvs_slic_d: bad arguments");
   int S = p->spixl_size;
   if (S < 6 || S > 96) return mvs::arg_fail("mvs_slic_d: spixl_size must be in [6, 96] (3S/16 > 0)");
   if (p->no_iter < 0) return mvs::arg_fail("mvs_slic_d: no_iter < 0");
+  if (p->edge_enable < 0 || p->edge_enable > 2) return mvs::arg_fail("mvs_slic_d: edge_enable must be 0, 1 or 2");
   // clSLIC ctor, clSLIC.cpp:15-18 (host float arithmetic)
   float xy = 1.0f / (1.4242f * (float)S);
   float col = 15.0f / (1.7321f * 128.0f);
@@ -219,13 +220,16 @@ int mvs_slic_d(mvs_ctx* c, const float* lab, int V, int W, int H, const mvs_slic
   col = col * col;
   hipStream_t s = c->stream;
   // one scratch for the update partials and the connectivity pass
+  // (the edge step's magnitude plane uses it before the first assignment)
   size_t sb = std::max(mvs::update_scratch_bytes(V, W, H, S),
                        p->enforce_connectivity ? sizeof(uint32_t) * (size_t)V * W * H : (size_t)0);
+  if (p->edge_enable) sb = std::max(sb, sizeof(float) * (size_t)V * W * H);
   int rc = 0;
   void* scr = sb ? mvs::scratch(c, sb, &rc) : nullptr;
   if (rc) return rc;
   float* part = mvs::update_scratch_bytes(V, W, H, S) ? (float*)scr : nullptr;
   RC(mvs::launch_init_centers(s, lab, V, W, H, S, spixl));
+  RC(mvs::launch_edge_step(s, lab, V, W, H, S, p->edge_enable, spixl, (float*)scr));
   if (part && S % 16 == 0) {
     // assign -> (update -> assign) x no_iter with each update's tile partials
     // produced by the assign pass before it (one Lab read per iteration)

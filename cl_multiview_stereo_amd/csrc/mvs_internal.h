@@ -66,6 +66,8 @@ constexpr int kLocal = 16;  // LOCAL_SIZE_UPDATE, header.h:37-38
 int launch_cvt(hipStream_t s, const uint8_t* rgbx, long npix, float* lab, uint8_t* l8);
 int launch_init_centers(hipStream_t s, const float* lab, int V, int W, int H, int S, float* spixl);
 int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labels);
+int launch_edge_step(hipStream_t s, float* lab, int V, int W, int H, int S, int edge_enable, float* spixl,
+                     float* edge);
 int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
                   float col_n, float weight, uint32_t* labels);
 size_t update_scratch_bytes(int V, int W, int H, int S);

@@ -94,6 +94,96 @@ __global__ void k_init_centers(const float4* __restrict__ lab, int W, int H, int
   o[6] = 0.0f;
 }
 
+// ---- edge_compute_alternative, clcode.cl:161-195 -------------------------
+// Magnitude of the reference's Sobel-like operator over the clamped 3x3
+// neighbourhood (its DX uses the centre c4 where a Sobel has c8: kept), left
+// to right without contraction; dot(v, 1) = (v.x + v.y) + v.z.  Written to
+// `edge` (the reference writes cvt_img in place while other work-items still
+// read it; here every read precedes the store pass k_edge_store).
+__global__ __launch_bounds__(256) void k_edge(const float4* __restrict__ lab, int W, int H,
+                                              float* __restrict__ edge) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= W) return;
+  const float4* L = lab + (long)z * W * H;
+  float4 c[9];
+#pragma unroll
+  for (int yo = -1; yo <= 1; yo++)
+#pragma unroll
+    for (int xo = -1; xo <= 1; xo++) {
+      const int xx = min(max(x + xo, 0), W - 1), yy = min(max(y + yo, 0), H - 1);
+      c[(yo + 1) * 3 + xo + 1] = L[(long)yy * W + xx];
+    }
+  auto mag2 = [&](float c0, float c1, float c2, float c3, float c4, float c5, float c6, float c7) {
+    float dx = -1.0f * c0 + c2;
+    dx = dx - 2.0f * c3;
+    dx = dx + 2.0f * c4;
+    dx = dx - c5;
+    dx = dx + c7;
+    float dy = -1.0f * c0 - 2.0f * c1;
+    dy = dy - c2;
+    dy = dy + c5;
+    dy = dy + 2.0f * c6;
+    dy = dy + c7;
+    const float dx2 = dx * dx, dy2 = dy * dy;
+    return dx2 + dy2;
+  };
+  const float sx = mag2(c[0].x, c[1].x, c[2].x, c[3].x, c[4].x, c[5].x, c[6].x, c[7].x);
+  const float sy = mag2(c[0].y, c[1].y, c[2].y, c[3].y, c[4].y, c[5].y, c[6].y, c[7].y);
+  const float sz = mag2(c[0].z, c[1].z, c[2].z, c[3].z, c[4].z, c[5].z, c[6].z, c[7].z);
+  edge[((long)z * H + y) * W + x] = sqrtf((sx * 1.0f + sy * 1.0f) + sz * 1.0f);
+}
+
+// edge_enable = 1: the magnitude lands in the Lab image as the reference's
+// float -> float3 store does (L, a, b <- e; the 4th float is untouched)
+__global__ __launch_bounds__(256) void k_edge_store(const float* __restrict__ edge, long n, float4* __restrict__ lab) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float e = edge[i];
+    float4 v = lab[i];
+    v.x = e;
+    v.y = e;
+    v.z = e;
+    lab[i] = v;
+  }
+}
+
+// ---- apply_edge_alternative, clcode.cl:204-248 ---------------------------
+// edge_enable = 2: each centre moves to its 8-neighbour of least edge value
+// (strict <, first in the reference's dxy order) and takes that pixel's
+// colour.  A centre outside the image (degenerate sizes) stays put.
+__global__ void k_apply_edge(const float4* __restrict__ lab, const float* __restrict__ edge, int W, int H, int mw,
+                             int mh, float* __restrict__ spixl) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x, row = blockIdx.y, z = blockIdx.z;
+  if (col >= mw) return;
+  float* sp = spixl + 8 * ((long)z * mw * mh + (long)row * mw + col);
+  const int cx = (int)sp[1], cy = (int)sp[2];
+  if (cx < 0 || cy < 0 || cx >= W || cy >= H) return;
+  const long P = (long)W * H;
+  const float* E = edge + z * P;
+  const int dxs[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, dys[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+  float ev = E[(long)cy * W + cx];
+  int bx = -1, by = -1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int nx = cx + dxs[i], ny = cy + dys[i];
+    if (nx >= 0 && ny >= 0 && nx < W && ny < H) {
+      const float ne = E[(long)ny * W + nx];
+      if (ne < ev) {
+        ev = ne;
+        bx = nx;
+        by = ny;
+      }
+    }
+  }
+  if (bx >= 0) {
+    const float4 c = lab[z * P + (long)by * W + bx];
+    sp[1] = (float)bx;
+    sp[2] = (float)by;
+    sp[3] = c.x;
+    sp[4] = c.y;
+    sp[5] = c.z;
+  }
+}
+
 // ---- init_label_per_pixl, clcode.cl:341-353 ------------------------------
 __global__ void k_grid_labels(int W, int H, int S, int mw, uint32_t* __restrict__ labels) {
   int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
@@ -519,6 +609,28 @@ int launch_init_centers(hipStream_t s, const float* lab, int V, int W, int H, in
   hipLaunchKernelGGL(k_init_centers, dim3((mw + 63) / 64, mh, V), dim3(64), 0, s, (const float4*)lab, W, H, S, mw,
                      mh, spixl);
   MVS_LAUNCH_CHECK("k_init_centers");
+  return 0;
+}
+
+// clSLIC::apply_edge_values (clSLIC.cpp:186-233); edge = V*W*H floats scratch
+int launch_edge_step(hipStream_t s, float* lab, int V, int W, int H, int S, int edge_enable, float* spixl,
+                     float* edge) {
+  if (edge_enable != 1 && edge_enable != 2) return 0;
+  hipLaunchKernelGGL(k_edge, dim3((W + 255) / 256, H, V), dim3(256), 0, s, (const float4*)lab, W, H, edge);
+  MVS_LAUNCH_CHECK("k_edge");
+  if (edge_enable == 1) {
+    // the reference's path: magnitude into the Lab image; apply_edge_alternative
+    // then reads the never-written edge_img (pinned as zeros): no centre moves
+    const long n = (long)V * W * H;
+    hipLaunchKernelGGL(k_edge_store, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, s, edge, n,
+                       (float4*)lab);
+    MVS_LAUNCH_CHECK("k_edge_store");
+    return 0;
+  }
+  const int mw = map_dim(W, S), mh = map_dim(H, S);
+  hipLaunchKernelGGL(k_apply_edge, dim3((mw + 63) / 64, mh, V), dim3(64), 0, s, (const float4*)lab, edge, W, H, mw,
+                     mh, spixl);
+  MVS_LAUNCH_CHECK("k_apply_edge");
   return 0;
 }
 

@@ -38,6 +38,7 @@ struct Settings {  // system_settings, clMVDE.cpp:14-36 defaults
   int array_width = 3, array_height = 3;
   int no_iter = 5;
   bool enforce_connectivity = false;
+  int edge_enable = 0;  // system_settings::edge_enable (header.h:61); 2 = the intended form (mvs.h)
   int neib_hor = 1, neib_ver = 1;
   int min_disp = 30, max_disp = 60, inc = 1;
   float bl_ratio = 1.03590f;
@@ -52,7 +53,7 @@ struct Settings {  // system_settings, clMVDE.cpp:14-36 defaults
 int usage() {
   std::fprintf(stderr,
                "usage: mvs_cli --data LIST --array WxH [--spixl-size S] [--color-weight w] [--no-iter n]\n"
-               "               [--connectivity] [--min-disp a] [--max-disp b] [--inc i] [--neib-hor h]\n"
+               "               [--connectivity] [--edge | --edge-intended] [--min-disp a] [--max-disp b] [--inc i] [--neib-hor h]\n"
                "               [--neib-ver v] [--bl-ratio r] [--kernel-size k] [--kernel-step s] [--fuse f]\n"
                "               [--gamma g] [--alpha a] [--no-prop p] [--final-state] [--filter] [--dump-init]\n"
                "               [--device d] [--out DIR] [--quiet]\n"
@@ -133,6 +134,8 @@ int main(int argc, char** argv) {
     else if (a == "--filter") st.filter = true;
     else if (a == "--dump-init") st.dump_init = true;
     else if (a == "--quiet") st.quiet = true;
+    else if (a == "--edge") st.edge_enable = 1;  // edge_enable = true, as the reference behaves
+    else if (a == "--edge-intended") st.edge_enable = 2;
     else if (!(v = val())) return usage();
     else if (a == "--data") st.data = v;
     else if (a == "--out") st.out = v;
@@ -202,7 +205,7 @@ int main(int argc, char** argv) {
   // ---- pipeline::perform_segmentation (pipeline.cpp:67-101) ----------------
   std::vector<float> lab(V * P * 4), spixl(V * M * 8, 0.0f);
   std::vector<uint32_t> labels(V * P);
-  mvs_slic_params sp{S, st.slic_color_weight, st.no_iter, st.enforce_connectivity ? 1 : 0};
+  mvs_slic_params sp{S, st.slic_color_weight, st.no_iter, st.enforce_connectivity ? 1 : 0, st.edge_enable};
   for (int v = 0; v < V; v++) {
     auto t0 = std::chrono::steady_clock::now();
     if (mvs_do_super_pixel_seg(ctx, imgs[v].rgbx.data(), W, H, &sp, &lab[v * P * 4], &spixl[v * M * 8],

@@ -54,6 +54,14 @@ typedef struct {
   float color_weight;        /* slic_color_weight (clMVDE.cpp:16 = 0.6) */
   int no_iter;               /* update/assign iterations (5) */
   int enforce_connectivity;  /* supress_local_lable x2 (clSLIC.cpp:373-411) */
+  int edge_enable;           /* apply_edge_values (clSLIC.cpp:84-86, 186-233; clcode.cl:161-248):
+                              * 0 off (the reference's default, header.h:61);
+                              * 1 the reference's path as it behaves: the edge magnitude
+                              *   overwrites the Lab image (L = a = b = e) and no centre moves
+                              *   (apply_edge_alternative reads the never-written edge_img,
+                              *   pinned as zeros);
+                              * 2 the intended path: Lab kept, each centre moves to its
+                              *   least-edge 8-neighbour and takes its colour. */
 } mvs_slic_params;
 
 /* Camera array / hypothesis set (pipeline::perform_depth_est).  Its arrays are
@@ -93,8 +101,10 @@ const char* mvs_version(void);
 int mvs_cvt_d(mvs_ctx* ctx, const uint8_t* rgbx, int V, int W, int H, float* lab, uint8_t* l8);
 
 /* SLIC on V views of lab (clSLIC::do_super_pixel_seg, clSLIC.cpp:67-122,
- * minus the cvt it starts with).  spixl [V][mh][mw][8], labels [V][H][W]. */
-int mvs_slic_d(mvs_ctx* ctx, const float* lab, int V, int W, int H, const mvs_slic_params* p,
+ * minus the cvt it starts with).  spixl [V][mh][mw][8], labels [V][H][W].
+ * lab is read only, except with p->edge_enable == 1, where the reference's
+ * edge step overwrites it (as clSLIC's lab_img_dev). */
+int mvs_slic_d(mvs_ctx* ctx, float* lab, int V, int W, int H, const mvs_slic_params* p,
                float* spixl, uint32_t* labels);
 
 /* SLIC-off grid mode: init_cluster_centers + init_label_per_pixl

@@ -222,14 +222,122 @@ void orc_suppress(const uint32_t* in, uint32_t* out, int W, int H) {
 }
 
 /* clSLIC::do_super_pixel_seg, clSLIC.cpp:67-122 (edge path disabled) */
+/* edge_compute_alternative, clcode.cl:161-195: a Sobel-like magnitude over the
+ * 3x3 clamped neighbourhood, colour index c = (yoff+1)*3 + (xoff+1).  The
+ * reference's DX uses c4 (the centre) where a Sobel would use c8, kept.
+ * Evaluated left to right, no contraction; dot(v, (1,1,1)) = (v.x + v.y) + v.z.
+ * The reference writes the result into cvt_img while other work-items still
+ * read it (a race); this restatement reads every neighbour before any write
+ * (the caller stores the result afterwards).  edge [H][W]. */
+void orc_edge(const float* lab, int W, int H, float* edge) {
+#pragma omp parallel for schedule(static)
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      float c[9][3];
+      int i = 0;
+      for (int yo = -1; yo <= 1; yo++)
+        for (int xo = -1; xo <= 1; xo++, i++) {
+          int xx = x + xo, yy = y + yo;
+          xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
+          yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
+          const float* p = lab + 4 * ((size_t)yy * W + xx);
+          c[i][0] = p[0];
+          c[i][1] = p[1];
+          c[i][2] = p[2];
+        }
+      float s[3];
+      for (int k = 0; k < 3; k++) {
+        float dx = -1.0f * c[0][k] + c[2][k];
+        dx = dx - 2.0f * c[3][k];
+        dx = dx + 2.0f * c[4][k];
+        dx = dx - c[5][k];
+        dx = dx + c[7][k];
+        float dy = -1.0f * c[0][k] - 2.0f * c[1][k];
+        dy = dy - c[2][k];
+        dy = dy + c[5][k];
+        dy = dy + 2.0f * c[6][k];
+        dy = dy + c[7][k];
+        const float dx2 = dx * dx, dy2 = dy * dy;
+        s[k] = dx2 + dy2;
+      }
+      edge[(size_t)y * W + x] = sqrtf((s[0] * 1.0f + s[1] * 1.0f) + s[2] * 1.0f);
+    }
+}
+
+/* apply_edge_alternative, clcode.cl:204-248: move each centre to the 8-
+ * neighbour of least edge value (strict <, first in the dxy order), taking
+ * that pixel's colour.  A centre outside the image (degenerate sizes) is left
+ * alone here; the reference would read out of bounds. */
+void orc_apply_edge(const float* lab, const float* edge, int W, int H, int S, float* spixl) {
+  static const int dxy[8][2] = {{-1, 0}, {-1, -1}, {0, -1}, {1, -1}, {1, 0}, {1, 1}, {0, 1}, {-1, 1}};
+  const int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
+  for (int s = 0; s < mw * mh; s++) {
+    float* sp = spixl + 8 * (size_t)s;
+    const int cx = (int)sp[1], cy = (int)sp[2];
+    if (cx < 0 || cy < 0 || cx >= W || cy >= H) continue;
+    float ev = edge[(size_t)cy * W + cx];
+    int changed = 0, bx = 0, by = 0;
+    for (int i = 0; i < 8; i++) {
+      const int nx = cx + dxy[i][0], ny = cy + dxy[i][1];
+      if (nx >= 0 && ny >= 0 && nx < W && ny < H) {
+        const float ne = edge[(size_t)ny * W + nx];
+        if (ne < ev) {
+          ev = ne;
+          bx = nx;
+          by = ny;
+          changed = 1;
+        }
+      }
+    }
+    if (changed) {
+      const float* c = lab + 4 * ((size_t)by * W + bx);
+      sp[1] = (float)bx;
+      sp[2] = (float)by;
+      sp[3] = c[0];
+      sp[4] = c[1];
+      sp[5] = c[2];
+    }
+  }
+}
+
+/* clSLIC::apply_edge_values (clSLIC.cpp:186-233), between init_cluster_centers
+ * and the first assignment (clSLIC.cpp:84-86).  edge_enable:
+ *   1  the reference's path as it behaves: the magnitude overwrites the Lab
+ *      image (L, a, b <- e, clcode.cl:194, a float stored to a float3), and
+ *      apply_edge_alternative reads edge_img, which nothing writes (an
+ *      uninitialised buffer, clSLIC.cpp:41) -- pinned as zeros, under which no
+ *      centre moves;
+ *   2  the intended path: the magnitude goes to edge_img, the Lab image is
+ *      kept, and the centres move to the least-edge 8-neighbour. */
+void orc_edge_step(float* lab, int W, int H, int S, int edge_enable, float* spixl) {
+  if (edge_enable != 1 && edge_enable != 2) return;
+  float* e = (float*)malloc(sizeof(float) * (size_t)W * H);
+  orc_edge(lab, W, H, e);
+  if (edge_enable == 1) {
+    for (size_t p = 0; p < (size_t)W * H; p++) lab[4 * p] = lab[4 * p + 1] = lab[4 * p + 2] = e[p];
+  } else {
+    orc_apply_edge(lab, e, W, H, S, spixl);
+  }
+  free(e);
+}
+
+void orc_slic_edge(const uint8_t* rgbx, int W, int H, int S, float weight, int no_iter, int enforce_conn,
+                   int edge_enable, float* lab, float* spixl, uint32_t* labels);
+
 void orc_slic(const uint8_t* rgbx, int W, int H, int S, float weight, int no_iter, int enforce_conn,
               float* lab, float* spixl, uint32_t* labels) {
+  orc_slic_edge(rgbx, W, H, S, weight, no_iter, enforce_conn, 0, lab, spixl, labels);
+}
+
+void orc_slic_edge(const uint8_t* rgbx, int W, int H, int S, float weight, int no_iter, int enforce_conn,
+                   int edge_enable, float* lab, float* spixl, uint32_t* labels) {
   float xy = 1.0f / (1.4242f * (float)S);
   float col = 15.0f / (1.7321f * 128.0f);
   xy = xy * xy;
   col = col * col;
   orc_cvt(rgbx, W, H, lab);
   orc_init_centers(lab, W, H, S, spixl);
+  orc_edge_step(lab, W, H, S, edge_enable, spixl);
   orc_assign(lab, spixl, W, H, S, xy, col, weight, labels);
   for (int i = 0; i < no_iter; i++) {
     orc_update(lab, labels, W, H, S, spixl);

@@ -72,17 +72,29 @@ def l8(lab):
     return out
 
 
-def slic(rgbx, S, weight=0.6, no_iter=5, enforce_connectivity=False):
-    """clSLIC::do_super_pixel_seg for ONE view -> (lab, spixl, labels)."""
+def slic(rgbx, S, weight=0.6, no_iter=5, enforce_connectivity=False, edge_enable=0):
+    """clSLIC::do_super_pixel_seg for ONE view -> (lab, spixl, labels).
+    edge_enable: 0 off, 1 the reference's apply_edge_values as it behaves
+    (Lab overwritten by the edge magnitude), 2 the intended form (centres moved
+    to the least-edge neighbour); orc_edge_step."""
     rgbx = np.ascontiguousarray(rgbx, np.uint8)
     H, W = rgbx.shape[:2]
     mw, mh = map_size(W, H, S)
     lab = np.zeros((H, W, 4), np.float32)
     sp = np.zeros((mh, mw, 8), np.float32)
     lb = np.zeros((H, W), np.uint32)
-    lib().orc_slic(_p(rgbx, u8p), W, H, S, _f(weight), no_iter, int(bool(enforce_connectivity)), _p(lab, f32p),
-                   _p(sp, f32p), _p(lb, u32p))
+    lib().orc_slic_edge(_p(rgbx, u8p), W, H, S, _f(weight), no_iter, int(bool(enforce_connectivity)),
+                        int(edge_enable), _p(lab, f32p), _p(sp, f32p), _p(lb, u32p))
     return lab, sp, lb
+
+
+def edge(lab):
+    """edge_compute_alternative magnitude [H][W] of ONE view (orc_edge)."""
+    lab = np.ascontiguousarray(lab, np.float32)
+    H, W = lab.shape[:2]
+    out = np.zeros((H, W), np.float32)
+    lib().orc_edge(_p(lab, f32p), W, H, _p(out, f32p))
+    return out
 
 
 def init_centers(lab, S):

@@ -313,3 +313,47 @@ def wta(vol, levels):
     # a pixel whose every cost is >= 1e6 keeps the default disparity 0
     none = best >= f32(1e6)
     return np.where(none, f32(0), disp), np.where(none, f32(0), conf)
+
+
+def edge(lab):
+    """edge_compute_alternative (clcode.cl:161-195): the magnitude of the
+    reference's Sobel-like operator (DX uses the centre c4), clamped 3x3
+    neighbourhood, float32 left to right; dot(v, 1) = (v.x + v.y) + v.z."""
+    lab = np.asarray(lab, np.float32)
+    H, W = lab.shape[:2]
+    ys = np.clip(np.arange(H)[:, None] + np.array([-1, 0, 1])[None, :], 0, H - 1)
+    xs = np.clip(np.arange(W)[:, None] + np.array([-1, 0, 1])[None, :], 0, W - 1)
+    c = [lab[ys[:, yo + 1]][:, xs[:, xo + 1], :3] for yo in (-1, 0, 1) for xo in (-1, 0, 1)]
+    f = np.float32
+    dx = f(-1) * c[0] + c[2]
+    dx = dx - f(2) * c[3]
+    dx = dx + f(2) * c[4]
+    dx = dx - c[5]
+    dx = dx + c[7]
+    dy = f(-1) * c[0] - f(2) * c[1]
+    dy = dy - c[2]
+    dy = dy + c[5]
+    dy = dy + f(2) * c[6]
+    dy = dy + c[7]
+    s = dx * dx + dy * dy
+    return np.sqrt((s[..., 0] + s[..., 1]) + s[..., 2]).astype(np.float32)
+
+
+def apply_edge(lab, e, spixl):
+    """apply_edge_alternative (clcode.cl:204-248) on one view's centres."""
+    H, W = e.shape
+    sp = np.array(spixl, np.float32, copy=True)
+    dxy = [(-1, 0), (-1, -1), (0, -1), (1, -1), (1, 0), (1, 1), (0, 1), (-1, 1)]
+    for s in sp.reshape(-1, 8):
+        cx, cy = int(s[1]), int(s[2])
+        if not (0 <= cx < W and 0 <= cy < H):
+            continue
+        ev, best = e[cy, cx], None
+        for ox, oy in dxy:
+            nx, ny = cx + ox, cy + oy
+            if 0 <= nx < W and 0 <= ny < H and e[ny, nx] < ev:
+                ev, best = e[ny, nx], (nx, ny)
+        if best is not None:
+            s[1], s[2] = best
+            s[3:6] = lab[best[1], best[0], :3]
+    return sp

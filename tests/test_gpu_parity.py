@@ -71,6 +71,25 @@ def test_slic(engine, name):
         assert_bits(sp[v][..., :7], osp[..., :7], f"spixl v{v}")
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("name", ["c3x1_s8", "c5x1_s32", "c2x1_s40"])
+def test_slic_edge(engine, name, mode):
+    """apply_edge_values (clSLIC.cpp:84-86, 186-233; clcode.cl:161-248):
+    mode 1 = the reference's path as it behaves (Lab overwritten in place by
+    the edge magnitude, no centre moved), mode 2 = the intended perturbation.
+    Lab, labels and centres bit-exact vs the oracle, both assignment paths."""
+    c = CASES[name]
+    b = build(c)
+    lab, _ = engine.cvt(dev(b["stack"]))
+    sp, lb = engine.slic(lab, c["S"], 0.6, 5, edge_enable=mode)
+    sp, lb, lab = sp.cpu().numpy(), as_u32(lb), lab.cpu().numpy()
+    for v in range(b["V"]):
+        olab, osp, olb = orc.slic(b["stack"][v], c["S"], 0.6, 5, edge_enable=mode)
+        assert_bits(lab[v], olab, f"lab v{v}")
+        assert_bits(lb[v], olb, f"labels v{v}")
+        assert_bits(sp[v][..., :7], osp[..., :7], f"spixl v{v}")
+
+
 @pytest.mark.parametrize("name", ["c3x1_s8", "c5x1_s32"])
 def test_slic_each_pass(engine, name):
     """Per-pass parity of the assign/update loop (no_iter = 0, 1, 2)."""
@@ -301,7 +320,7 @@ def test_host_api_matches_device_api(engine):
     lab = np.zeros((H, W, 4), np.float32)
     sp = np.zeros((mh, mw, 8), np.float32)
     lb = np.zeros((H, W), np.uint32)
-    p = _lib.SlicParams(c["S"], 0.6, 5, 0)
+    p = _lib.SlicParams(c["S"], 0.6, 5, 0, 0)
     _lib.check(engine.L.mvs_do_super_pixel_seg(engine.ctx, img.ctypes.data_as(C.c_void_p), W, H, C.byref(p),
                                                lab.ctypes.data_as(C.c_void_p), sp.ctypes.data_as(C.c_void_p),
                                                lb.ctypes.data_as(C.c_void_p)), "mvs_do_super_pixel_seg")

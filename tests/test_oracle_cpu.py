@@ -10,6 +10,7 @@ import math
 import numpy as np
 import pytest
 
+import np_ref
 import oracle.oracle as orc
 from cases import CASES, PIXEL_CASES, build
 from np_ref import (fma32, assign, boundary, cvt_f64, grid_labels, l8, ncc_volume, suppress, sweep_pixel_sad, update,
@@ -302,3 +303,37 @@ def test_fused_wta_fold_equals_top4(D, nw):
     fd, fc = _fused_wta_model(vol, levels, nw)
     assert np.array_equal(fd.view(np.uint32), od.view(np.uint32))
     assert np.array_equal(fc.view(np.uint32), oc.view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_edge_magnitude_bit_exact(seed):
+    """orc_edge (edge_compute_alternative, clcode.cl:161-195) against the
+    numpy restatement, image borders included."""
+    rng = np.random.default_rng(seed)
+    rgbx = rng.integers(0, 256, (23, 37, 4), dtype=np.uint8)
+    lab = orc.cvt(rgbx)
+    assert np.array_equal(orc.edge(lab).view(np.uint32), np_ref.edge(lab).view(np.uint32))
+
+
+@pytest.mark.parametrize("S", [8, 12])
+def test_slic_edge_modes(S):
+    """apply_edge_values between init_cluster_centers and the first assignment
+    (clSLIC.cpp:84-86): mode 1 overwrites Lab with the magnitude and moves no
+    centre; mode 2 keeps Lab and moves each centre to its least-edge
+    neighbour (numpy restatement)."""
+    from cl_multiview_stereo_amd import synth
+    stack, _ = synth.make_stack(70, 45, 1, 1, 0, 7, 1.0, S)
+    lab0 = orc.cvt(stack[0])
+    e = np_ref.edge(lab0)
+    lab1, _, _ = orc.slic(stack[0], S, 0.6, 0, edge_enable=1)
+    assert np.array_equal(lab1[..., 0], e) and np.array_equal(lab1[..., 1], e) and np.array_equal(lab1[..., 2], e)
+    _, sp1, lb1 = orc.slic(stack[0], S, 0.6, 0, edge_enable=1)
+    init = orc.init_centers(lab0, S)
+    assert np.array_equal(sp1[..., :6], init[..., :6])  # no centre moves (edge_img never written)
+    assert np.array_equal(lb1, orc.assign(lab1, init, S))
+    lab2, sp2, lb2 = orc.slic(stack[0], S, 0.6, 0, edge_enable=2)
+    assert np.array_equal(lab2, lab0)
+    moved = np_ref.apply_edge(lab0, e, init)
+    assert np.array_equal(sp2[..., :6], moved[..., :6])
+    assert (moved[..., 1:3] != init[..., 1:3]).any()
+    assert np.array_equal(lb2, orc.assign(lab0, moved, S))

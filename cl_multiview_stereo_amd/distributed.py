@@ -11,9 +11,13 @@ exchange exactly what later stages read from other views:
   cvt (a1), block + its neighbours  -                         none (every rank holds the
                                                               RGBx stack; converts only
                                                               the views its block reads)
-  SLIC (a2-a6), own block           -                         all-gather spixl + labels
+  SLIC (a2-a6), own block           -                         all-gather labels, issued
+                                                              here and waited for only
+                                                              before refinement: it runs
+                                                              beside the sweeps below
   boundary (a8), own block          -                         none
-  superpixel sweep (a9), own block  Lab of neighbours         all-gather spixl (s7 = seed)
+  superpixel sweep (a9), own block  Lab of neighbours         all-gather spixl (s7 = seed),
+                                                              after the per-pixel sweep
   per-pixel NCC + WTA, own block    l8 / window planes of     none until the filter
                                     neighbours (built for the
                                     block + neighbours only)
@@ -81,6 +85,21 @@ class ViewGather:
     def block(self) -> tuple[int, int]:
         return self.blocks[self.rank]
 
+    def start(self, local: torch.Tensor, full: torch.Tensor) -> "PendingGather":
+        """The same all-gather, asynchronous: the collective is issued behind the
+        work already on the current stream, later work on the stream runs beside
+        it, and PendingGather.wait() makes the stream wait for it.  `local`
+        must be `full`'s own block (in place)."""
+        z0, z1 = self.block
+        if local.shape[0] != z1 - z0 or full.shape[0] != self.V:
+            raise ValueError(f"rank {self.rank}: bad block / full shapes")
+        if self.world == 1 or not self.equal:
+            return PendingGather(self(local, full))
+        if local.data_ptr() != full[z0:z1].data_ptr():
+            full[z0:z1] = local
+        work = dist.all_gather_into_tensor(full, full[z0:z1], group=self.group, async_op=True)
+        return PendingGather(full, work)
+
     def __call__(self, local: torch.Tensor, full: torch.Tensor | None = None) -> torch.Tensor:
         z0, z1 = self.block
         if local.shape[0] != z1 - z0:
@@ -105,6 +124,24 @@ class ViewGather:
         for (b0, b1), buf in zip(self.blocks, bufs):
             full[b0:b1] = buf[:b1 - b0]
         return full
+
+
+class PendingGather:
+    def __init__(self, full: torch.Tensor, work=None):
+        self.full, self.work = full, work
+
+    def wait(self) -> torch.Tensor:
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        return self.full
+
+
+def _expand(blk: torch.Tensor, V: int, z0: int) -> torch.Tensor:
+    """[V, ...] zeros holding `blk` at views [z0, z0 + len(blk))."""
+    full = blk.new_zeros((V,) + tuple(blk.shape[1:]))
+    full[z0:z0 + blk.shape[0]] = blk
+    return full
 
 
 @dataclass
@@ -139,14 +176,19 @@ class ShardedPipeline:
         need = self.cam.views_needed(z0, z1)
         lab, l8 = b.cvt(rgbx, need)
         sp_blk, lb_blk = b.slic(lab[z0:z1], S, st.slic_color_weight, st.no_iter, st.enforce_connectivity)
-        spixl = g(sp_blk)
-        labels = g(lb_blk)
-        rep = b.boundary(spixl, labels, S, z0, z1)
+        spixl = _expand(sp_blk, V, z0)
+        labels = _expand(lb_blk, V, z0)
+        # the labels (4 B/px/view, the largest gather) are read from other views
+        # only by the refinement: in flight while this rank sweeps its block
+        pending = g.start(labels[z0:z1], labels)
+        rep = b.boundary(spixl, labels, S, z0, z1)  # own block only
         b.sweep_spixl(lab, spixl, rep, self.cam, S, z0, z1)
-        spixl = g(spixl[z0:z1], spixl)
         out = ShardOutput(z0, z1, spixl, labels)
         if self.pixel_cost:
             out.disp, out.conf = b.pixel_sweep(lab, l8, self.cam, z0, z1, self.pixel_cost, st.window, need)
+        out.spixl = g(spixl[z0:z1], spixl)  # centres + seeds (s7) of every view
+        out.labels = pending.wait()
+        spixl, labels = out.spixl, out.labels
         if self.refine:
             out.disp_refined = self._refine(spixl, labels, rep, z0, z1)
         if self.filt:

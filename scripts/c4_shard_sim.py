@@ -53,6 +53,10 @@ class ReplayGather:
     def block(self):
         return self.blocks[self.rank]
 
+    def start(self, local, full):
+        from cl_multiview_stereo_amd.distributed import PendingGather
+        return PendingGather(self(local, full))
+
     def __call__(self, local, full=None):
         z0, z1 = self.block
         rec = self.rec[self.i % len(self.rec)]

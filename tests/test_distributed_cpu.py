@@ -118,3 +118,32 @@ def test_gather_single_process_is_copy():
     assert torch.equal(g(x), x)
     with pytest.raises(ValueError):
         g(x[:2])
+
+
+def _gather_worker(rank, world, port, outdir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from cl_multiview_stereo_amd.distributed import ViewGather
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = ViewGather(4 * world)
+        z0, z1 = g.block
+        full = torch.full((4 * world, 5), -1.0)
+        full[z0:z1] = torch.arange(20.0).reshape(4, 5) + 100 * rank
+        pend = g.start(full[z0:z1], full)  # async, in place (all_gather_into_tensor, async_op=True)
+        got = pend.wait()
+        assert got.data_ptr() == full.data_ptr() and pend.wait() is full
+        np.save(os.path.join(outdir, f"g{rank}.npy"), got.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_async_gather_gloo():
+    """ViewGather.start (the labels all-gather the sharded pipeline overlaps
+    with its sweeps) equals the blocks of every rank, world 2."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_gather_worker, args=(2, _free_port(), d), nprocs=2, join=True, start_method="spawn")
+        want = np.concatenate([np.arange(20.0).reshape(4, 5) + 100 * r for r in range(2)]).astype(np.float32)
+        for r in range(2):
+            assert np.array_equal(np.load(os.path.join(d, f"g{r}.npy")), want)

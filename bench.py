@@ -435,7 +435,7 @@ def view_sharded(args, e, world, rank, sync):
     V, W, H = c["aw"] * c["ah"], c["W"], c["H"]
     st = params.Settings(spixl_size=c["S"], array_width=c["aw"], array_height=c["ah"], min_disp=c["dmin"],
                          max_disp=c["dmax"], inc=1, bl_ratio=c["bl"], window=c["K"], cost="ncc")
-    stack, _ = synth.make_stack(W, H, c["aw"], c["ah"], c["dmin"], c["dmax"], c["bl"], 0x5EED + 4)
+    stack, _ = synth.make_stack(W, H, c["aw"], c["ah"], c["dmin"], c["dmax"], c["bl"], 0x5EED + 2)  # = --config c4
     rgbx = torch.from_numpy(stack).to(e.device)
     mat, num = params.flatten_subsets(params.nearest_neighbours(c["aw"], c["ah"], c["knn"]))
     cam = CameraArray(c["aw"], c["bl"], params.disparity_levels(c["dmin"], c["dmax"], 1), mat, num)

@@ -920,6 +920,150 @@ __global__ __launch_bounds__(256) void k_remove_incons_px(const float* __restric
   }
 }
 
+// The same answer with the per-pixel preparation shared through LDS.  The
+// walk over candidates is a chain of dependent gather round trips, so the
+// kernel is latency-bound: k_remove_incons_px keeps 96 candidate registers
+// per thread (144 VGPRs, 3 waves per SIMD) and walks a shard's references one
+// after another.  Here a workgroup is 64 pixels of a row x RG references: the
+// reference-independent part -- the V proj values, their descending sort and
+// each candidate's first stability term -- is computed once into LDS by the
+// RG waves together, then wave w walks the candidates of reference
+// z0 + RG * blockIdx.z + w from LDS with a handful of registers.
+constexpr int RI_MAXV = 32;
+template <int RG, int FB, int CP>
+__global__ __launch_bounds__(64 * RG) void k_remove_incons_lds(const float* __restrict__ proj,
+                                                               const float* __restrict__ full, int V, int W, int H,
+                                                               int aw, float bl, float fuse, int z0, int z1,
+                                                               float* __restrict__ out) {
+  __shared__ float s_pv[RI_MAXV][64];  // proj values at the pixel, per view
+  __shared__ float s_sv[RI_MAXV][64];  // candidates sorted descending (-inf: none)
+  __shared__ float s_a[RI_MAXV][64];   // first stability term of each sorted candidate
+  __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int x = blockIdx.x * 64 + lane, y = blockIdx.y;
+  const bool xin = x < W;
+  const long P = (long)W * H, p = (long)y * W + (xin ? x : 0);
+  for (int j = wave; j < RI_MAXV; j += RG) s_pv[j][lane] = (xin && j < V) ? proj[P * j + p] : 0.0f;
+  {
+    const int r = z0 + RG * blockIdx.z + wave;
+    if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the walk evaluates them
+      s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float sv[RI_MAXV];
+#pragma unroll
+    for (int j = 0; j < RI_MAXV; j++) {
+      const float v = s_pv[j][lane];
+      sv[j] = v != 0 ? v : -INFINITY;  // non-candidates sort last
+    }
+    sort_desc<RI_MAXV>(sv);
+#pragma unroll
+    for (int j = 0; j < RI_MAXV; j++) s_sv[j][lane] = sv[j];
+  }
+  __syncthreads();
+  for (int k = wave; k < RI_MAXV; k += RG) {
+    const float d = s_sv[k][lane];
+    float a = 0.0f;
+    for (int j = 0; j < V; j++) {
+      const float pj = s_pv[j][lane];
+      if (pj != 0) {
+        const float diff = pj - d;
+        if (fabsf(diff) > fuse) a = a - 1.0f;
+        if (fabsf(diff) <= fuse) a = a + 1.0f;
+      }
+    }
+    s_a[k][lane] = a;
+  }
+  __syncthreads();
+  const int r = z0 + RG * blockIdx.z + wave;
+  if (r >= z1 || !xin) return;  // after the last barrier
+  const float xf = (float)x, yf = (float)y;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)full, 0, 0x7fffffff, 0x00020000);
+  // the next distinct candidate (views holding the same d: one evaluation)
+  int k = 0;
+  float prev = __int_as_float(0x7fc00000);
+  auto next = [&](float& d, float& a) -> bool {
+    while (k < V) {
+      d = s_sv[k][lane];
+      a = s_a[k][lane];
+      k++;
+      if (d == -INFINITY) {  // no candidates left
+        k = V;
+        return false;
+      }
+      const bool dup = d == prev;
+      prev = d;
+      if (!dup) return true;
+    }
+    return false;
+  };
+  // CP candidates are evaluated together (their gathers in flight at once):
+  // the later ones only matter when the earlier are unstable, which is the
+  // common case; the answer is still the first stable one in order
+  float dest = 0.0f;
+  while (true) {
+    float d[CP], st[CP], bd[CP];
+    bool has[CP];
+#pragma unroll
+    for (int c = 0; c < CP; c++) {
+      has[c] = next(d[c], st[c]);
+      bd[c] = bl * d[c];
+    }
+    if (!has[0]) break;
+    for (int j0 = 0; j0 < V; j0 += FB) {
+      // each remaining view adds at most +1: a candidate stops once stab >= 0
+      // is out of reach (stab counts exactly, so this only skips work)
+      bool live[CP], any = false;
+#pragma unroll
+      for (int c = 0; c < CP; c++) {
+        live[c] = has[c] && st[c] + (float)(V - j0) >= 0.0f;
+        any = any || live[c];
+      }
+      if (!any) break;
+      float dc[CP][FB];
+      bool in[CP][FB];
+#pragma unroll
+      for (int u = 0; u < FB; u++) {
+        const int j = j0 + u;
+        const float2 o = s_off[wave][j < V ? j : 0];  // wave-uniform: an LDS broadcast
+#pragma unroll
+        for (int c = 0; c < CP; c++) {
+          const int xx = (int)(xf - roundf(d[c] * o.x));
+          const int yy = (int)(yf - roundf(bd[c] * o.y));
+          in[c][u] = live[c] && j < V && (unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H;
+          // 32-bit byte offsets (the stack is < 2 GB: the launcher checks): the view
+          // base is scalar, the in-view offset one integer multiply-add.  Every
+          // lane issues its load -- a skipped tap gets an offset past the buffer
+          // and reads 0 -- so no branch splits the block's gathers and they all
+          // stay in flight together (a branch made the compiler wait on each)
+          const int off = in[c][u] ? (yy * W + xx) * 4 : 0x7fffffff;
+          dc[c][u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, (int)(P * j * 4), 0));
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CP; c++)
+#pragma unroll
+        for (int u = 0; u < FB; u++) {
+          if (in[c][u]) {
+            const float diff = dc[c][u] - d[c];
+            if (fabsf(diff) > fuse) st[c] = st[c] - 1.0f;
+            if (fabsf(diff) < fuse) st[c] = st[c] + 1.0f;
+          }
+        }
+    }
+    bool done = false;
+#pragma unroll
+    for (int c = 0; c < CP; c++)
+      if (!done && has[c] && st[c] >= 0) {
+        dest = d[c];
+        done = true;
+      }
+    if (done || !has[CP - 1]) break;
+  }
+  out[P * r + p] = dest;
+}
+
 }  // namespace
 
 int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
@@ -986,7 +1130,25 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
     else if (V <= 16)
       hipLaunchKernelGGL((k_remove_incons_px<16, 8>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1,
                          out);
-    else if (V <= 32) {
+    else if (V <= 32 && (long)V * W * H * 4 < (1L << 31) &&
+             !(getenv("MVS_FILTER_KERNEL") && std::string(getenv("MVS_FILTER_KERNEL")) == "px")) {
+      // shared-preparation form, 32-bit gather offsets (MVS_FILTER_KERNEL=px:
+      // the per-pixel form below)
+      constexpr int RG = 4;
+      const dim3 gl((W + 63) / 64, H, (z1 - z0 + RG - 1) / RG);
+      // MVS_FILTER_CP: candidates evaluated together (1 | 2 | 3; A/B, read per call)
+      const char* cp = getenv("MVS_FILTER_CP");
+      const int ncp = cp ? atoi(cp) : 2;
+      if (ncp == 1)
+        hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 1>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, fuse,
+                           z0, z1, out);
+      else if (ncp == 3)
+        hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 3>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, fuse,
+                           z0, z1, out);
+      else
+        hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 2>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, fuse,
+                           z0, z1, out);
+    } else if (V <= 32) {
       // MVS_FILTER_FB: views per gather block (A/B; read per call).  Measured at
       // C4 (scripts/bench_filter.py): blocks of 8 gathers 54 ms for all 32
       // references, 4: 35 ms, 2: 35 ms -- a candidate's early exit comes after

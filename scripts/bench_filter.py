@@ -20,12 +20,12 @@ from cl_multiview_stereo_amd.pipeline import Pipeline  # noqa: E402
 
 
 def main():
-    variants = sys.argv[1:] or ["MVS_FILTER_FB=8", "MVS_FILTER_FB=4", "MVS_FILTER_FB=2"]
+    variants = sys.argv[1:] or ["MVS_FILTER_KERNEL=px", "MVS_FILTER_KERNEL=lds"]
     aw, ah, W, H = 8, 4, 1920, 1080
     e = Engine(0)
     st = params.Settings(spixl_size=32, array_width=aw, array_height=ah, min_disp=0, max_disp=127, inc=1, neib_hor=0,
                          neib_ver=0, bl_ratio=1.0, window=5, cost="ncc")
-    stack, _ = synth.make_stack(W, H, aw, ah, 0, 127, 1.0, 0x5EED + 4)
+    stack, _ = synth.make_stack(W, H, aw, ah, 0, 127, 1.0, 0x5EED + 2)
     rgbx = torch.from_numpy(stack).cuda()
     pipe = Pipeline(e, st, W, H, view_subset=params.nearest_neighbours(aw, ah, 5), pixel_cost="ncc", refine=True,
                     fused=True)

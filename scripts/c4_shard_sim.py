@@ -91,7 +91,7 @@ def main():
     e = Engine(0)
     st = params.Settings(spixl_size=32, array_width=aw, array_height=ah, min_disp=0, max_disp=127, inc=1, bl_ratio=1.0,
                          window=5, cost="ncc")
-    stack, _ = synth.make_stack(W, H, aw, ah, 0, 127, 1.0, 0x5EED + 4)
+    stack, _ = synth.make_stack(W, H, aw, ah, 0, 127, 1.0, 0x5EED + 2)
     rgbx = torch.from_numpy(stack).cuda()
     mat, num = params.flatten_subsets(params.nearest_neighbours(aw, ah, 5))
     cam = CameraArray(aw, 1.0, params.disparity_levels(0, 127, 1), mat, num)

@@ -60,7 +60,8 @@ CONFIGS = {
 METRIC = "Mpix/s depth (1080p, 128 depth hyp, 5 views) + depth L1 vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK = 1024 * 2.4e9 / 4.0  # wave64 VALU instructions/s: 1024 SIMDs x 2.4 GHz / 4 cycles
-SAD_SAMPLE_ROWS = 640  # CPU-baseline band of the per-pixel SAD sweep (cpu_baseline)
+CPU_SAMPLE_SECONDS = 15.0  # target CPU time of the per-pixel sweep's sampled row band (cpu_baseline)
+CPU_TAP_RATE = {"ncc": 13e9, "sad": 8e9}  # oracle taps/s on the GPU box's 16 host threads (measured r02)
 
 
 def log(*a):
@@ -215,7 +216,7 @@ def _cpu_info():
 
 def _pmc_traffic(name, W, H, D):
     """Corrected HBM bytes per launch of k_wta from this configuration's own
-    PMC pass (profiles/pmc_wta_<config>.json, written by scripts/pmc_wta.sh),
+    PMC pass (profiles/pmc_wta_<config>.json, written by scripts/profile.sh),
     or None when no pass of this exact shape exists."""
     p = os.path.join(ROOT, "profiles", f"pmc_wta_{name}.json")
     if not os.path.exists(p):
@@ -229,14 +230,18 @@ def _pmc_traffic(name, W, H, D):
     return j.get("hbm_bytes_per_launch")
 
 
-def _valu_insts(name, cost, fused):
-    """SQ_INSTS_VALU per launch of the NCC sweep (profiles/pmc_ncc.json, C2),
-    launch-weighted over the band-width variants."""
-    pmc_ncc = os.path.join(ROOT, "profiles", "pmc_ncc.json")
-    if name != "c2" or cost != "ncc" or not os.path.exists(pmc_ncc):
+def _valu_insts(name, cost, fused, W, H, D):
+    """SQ_INSTS_VALU per launch of the NCC sweep from this configuration's own
+    PMC pass (profiles/pmc_ncc_<config>.json, scripts/profile.sh), launch-
+    weighted over the band-width variants; None without a pass of this shape."""
+    pmc_ncc = os.path.join(ROOT, "profiles", f"pmc_ncc_{name}.json")
+    if cost != "ncc" or not os.path.exists(pmc_ncc):
+        return None
+    j = json.load(open(pmc_ncc))
+    if (j.get("W"), j.get("H"), j.get("D")) != (W, H, D):
         return None
     tag = "true>" if fused else "false>"
-    ent = [v for k, v in json.load(open(pmc_ncc)).items() if k.startswith("k_ncc_volume") and k.endswith(tag)]
+    ent = [v for k, v in j.items() if k.startswith("k_ncc_volume") and k.endswith(tag)]
     if not ent:
         return None
     wts = [e.get("launches", 1) for e in ent]
@@ -341,7 +346,7 @@ def bench(args, world, rank, local):
         t_f = avg(head_timers["fused"])
         cells = float(D) * W * H
         nbr = max(1, int(pipe.cam.subset_num[0]))
-        insts = _valu_insts(args.config, cost, True)
+        insts = _valu_insts(args.config, cost, True, W, H, D)
         res["roofline_sweep"] = {
             "kernel": "k_ncc_volume<..., FUSE=true> (sweep + WTA, the headline step's dominant kernel)",
             "bound": "valu", "avg_launch_ms": round(t_f * 1e3, 4),
@@ -385,7 +390,7 @@ def bench(args, world, rank, local):
                   "view_cells_per_s": round(cells * nbr / t_ncc / 1e9, 3), "unit_view_cells": "G view-cells/s",
                   "hbm_write_GBps": round(4.0 * cells / t_ncc / 1e9, 1),
                   "hbm_write_frac": round(4.0 * cells / t_ncc / 1e9 / HBM_PEAK_GBS, 4)}
-            insts = _valu_insts(args.config, cost, False)
+            insts = _valu_insts(args.config, cost, False, W, H, D)
             if insts is not None:
                 sw.update({"bound": "valu", "valu_wave_insts_per_launch": round(insts),
                            "valu_issue_frac": round(insts / t_ncc / VALU_PEAK, 4)})
@@ -473,34 +478,41 @@ def cpu_baseline(pipe, stack, cfg, cost, out):
     sp = orc.sweep(lab_all, sp, rep, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"], S)
     t_seg = time.perf_counter() - t0
     maps = {}
-    if cost == "ncc":
-        q = orc.l8(lab_all)
-        maps["disp"] = np.stack([orc.wta(orc.ncc_volume(q, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"],
-                                                        cfg["bl"], cfg["K"], z), cam.levels)[0] for z in range(V)])
-    elif cost == "sad":
-        # ~160 s per 1080p view per core at D=128: time a band of rows.  With
-        # horizontal-only neighbours (every dy = 0) a pixel's taps and
-        # projections stay within rows y-2..y+2, so the band's rows above its
-        # last 2 are exactly the full image's rows.
+    rows, t_band = H, None
+    if cost in ("ncc", "sad"):
+        # the per-pixel sweep: a row band when the whole step would take the
+        # host much longer than CPU_SAMPLE_SECONDS (SAD at D=128: ~160 s per
+        # 1080p view per core; C5's NCC 7x7 at D=256: ~4 min on 16 threads).
+        # With horizontal-only neighbours (every dy = 0) a pixel's window taps
+        # and projections stay within rows y-R..y+R, so the band's rows above
+        # its last R are exactly the full image's rows.
         horizontal = all(int(cam.view_subset[z, n]) // cfg["aw"] == z // cfg["aw"]
                          for z in range(V) for n in range(int(cam.subset_num[z])))
-        rows = SAD_SAMPLE_ROWS if horizontal and H > SAD_SAMPLE_ROWS else H
+        K = cfg["K"] if cost == "ncc" else 5
+        per_row = V * W * len(cam.levels) * max(1, int(cam.subset_num.max())) * K * K
+        want = int(CPU_SAMPLE_SECONDS * CPU_TAP_RATE[cost] / per_row)
+        rows = H if (not horizontal or want >= H) else max(64, want)
+        lab_band = np.ascontiguousarray(lab_all[:, :rows])
         t1 = time.perf_counter()
-        band = orc.sweep_pixel_sad(np.ascontiguousarray(lab_all[:, :rows]), cam.levels, cam.view_subset,
-                                   cam.subset_num, cfg["aw"], cfg["bl"])
+        if cost == "ncc":
+            q = orc.l8(lab_band)
+            band = np.stack([orc.wta(orc.ncc_volume(q, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"],
+                                                    cfg["bl"], K, z), cam.levels)[0] for z in range(V)])
+        else:
+            band = orc.sweep_pixel_sad(lab_band, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"])
         t_band = time.perf_counter() - t1
-        keep = rows if rows == H else rows - 2
-        maps["disp"] = (band[:, :keep], keep)
+        keep = rows if rows == H else rows - K // 2
+        maps["disp"] = (band[:, :keep], keep) if rows != H else band
     if cfg.get("refine"):
         maps["disp_refined"] = orc.refine(sp, lb, rep, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"],
                                           S)["disp"]
         if cfg.get("filt"):
             maps["disp_filtered"] = orc.filt(maps["disp_refined"], cfg["aw"], cfg["bl"], 1.0)[1]
     t_all = time.perf_counter() - t0
-    if cost == "sad" and maps["disp"][1] != H:
-        rows = maps["disp"][1] + 2
+    if rows != H:
         cpu = {"value": round(V * W * rows / t_band / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
-               "sample": f"the per-pixel SAD sweep of rows 0..{rows - 1} of all {V} reference views ({W} wide, "
+               "sample": f"the per-pixel {cost.upper()} sweep + WTA of rows 0..{rows - 1} of all {V} reference views "
+                         f"({W} wide, "
                          f"{len(cam.levels)} hypotheses x {int(cam.subset_num.max())} neighbours) on "
                          f"oracle/mvs_oracle.c, OpenMP x{threads}: {t_band:.1f}s (segmentation of the full views, "
                          f"{t_seg:.1f}s, not counted)",
@@ -517,7 +529,7 @@ def cpu_baseline(pipe, stack, cfg, cost, out):
     sample = f"the last timed step's disparity maps, all {V} reference views, {W}x{H}"
     for k, od in maps.items():
         gd = getattr(out, k).cpu().numpy()
-        if isinstance(od, tuple):  # a row band (the SAD sample)
+        if isinstance(od, tuple):  # a row band (the per-pixel sweep's sample)
             od, keep = od
             gd = gd[:, :keep]
             sample = (f"rows 0..{keep - 1} (the CPU sample's exact rows) of the last timed step's disparity maps, "

@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output (rocpd SQLite) into profiles/<tag>_*.
 
-    python scripts/summarize_prof.py <prof_dir> <tag>
+    python scripts/summarize_prof.py <prof_dir> <tag> [<config>]
 
 <prof_dir>/trace/*.db     --kernel-trace --stats   -> <tag>_kernel_stats.csv
 <prof_dir>/pmc_fetch/*.db --pmc FETCH_SIZE          \
-<prof_dir>/pmc_write/*.db --pmc WRITE_SIZE          -> <tag>_pmc.json, pmc_wta.json
+<prof_dir>/pmc_write/*.db --pmc WRITE_SIZE          -> <tag>_pmc.json, pmc_wta_<config>.json
+<prof_dir>/pmc_valu/*.db  --pmc SQ_INSTS_VALU ...   -> pmc_ncc_<config>.json
+(bench.py reads pmc_wta_<config>.json / pmc_ncc_<config>.json for the run's
+own configuration only, shape-checked against <prof_dir>/trace_bench.json.)
 FETCH_SIZE on gfx950 counts 128-B requests at 64 B for wide coalesced streaming
 reads: it is doubled (MI355X_MICROARCH.md, HBM section).  WRITE_SIZE is exact
 for 16-B-per-lane streaming stores.
@@ -33,6 +36,13 @@ def short(name):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
+    cfg = sys.argv[3] if len(sys.argv) > 3 else "c2"
+    shape = {}
+    try:
+        b = json.load(open(os.path.join(src, "trace_bench.json")))
+        shape = {"W": b["config"]["width"], "H": b["config"]["height"], "D": b["config"]["hypotheses"]}
+    except (OSError, ValueError, KeyError):
+        pass
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     c = db(os.path.join(src, "trace"))
@@ -67,15 +77,16 @@ def main():
     if wta:
         json.dump({"kernel": wta, "source": f"profiles/{tag}_pmc.json",
                    "hbm_bytes_per_launch": pmc[wta]["hbm_bytes_per_launch"],
-                   "note": "2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes"},
-                  open(os.path.join(out, "pmc_wta.json"), "w"), indent=1)
+                   "note": "2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes", "config": cfg, **shape},
+                  open(os.path.join(out, f"pmc_wta_{cfg}.json"), "w"), indent=1)
     ncc = [k for k in sorted(pmc) if k.startswith("k_ncc_volume") and "SQ_INSTS_VALU_per_launch" in pmc[k]]
     if ncc:
         json.dump({k: {"valu_wave_insts_per_launch": pmc[k]["SQ_INSTS_VALU_per_launch"],
                        "lds_wave_insts_per_launch": pmc[k].get("SQ_INSTS_LDS_per_launch"),
                        "launches": pmc[k]["launches"]} for k in ncc} |
-                  {"source": f"profiles/{tag}_pmc.json", "note": "SQ_INSTS_VALU / SQ_INSTS_LDS, own --pmc pass"},
-                  open(os.path.join(out, "pmc_ncc.json"), "w"), indent=1)
+                  {"source": f"profiles/{tag}_pmc.json", "note": "SQ_INSTS_VALU / SQ_INSTS_LDS, own --pmc pass",
+                   "config": cfg, **shape},
+                  open(os.path.join(out, f"pmc_ncc_{cfg}.json"), "w"), indent=1)
     for r in rows[:8]:
         print(f"{short(r[0]):40s} calls={r[1]:5d} avg={r[3]:9.3f} us  {r[4]:6.2f}%")
     for k in sorted(pmc):

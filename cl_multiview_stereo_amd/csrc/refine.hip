@@ -1064,6 +1064,340 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_lds(const float* __re
   out[P * r + p] = dest;
 }
 
+// roundf(v) as truncf(v + copysignf(0.49999997f, v)): equal for every non-NaN
+// float (checked exhaustively over all 2^32 encodings, tests/test_oracle_cpu.py
+// test_round_half_away_identity); 3 VALU instead of ~6.  NaN stays NaN.
+__device__ __forceinline__ float round_ha(float v) {
+  return truncf(v + copysignf(__int_as_float(0x3effffff), v));
+}
+
+// The same answer with one work queue per lane.  k_remove_incons_lds walks
+// candidates in lock-step: a wave runs every candidate until the LAST of its
+// 64 lanes has given it up, so it pays, per candidate, the longest of the 64
+// walks (measured at C4: 31.4 candidate rounds per wave against 20.5 per
+// pixel, and most of a round's gather blocks idle).  Here each lane carries
+// its own walk state and every pass of the loop does one gather block per
+// slot: a lane whose candidate dies takes its next one in the next pass, so a
+// wave runs the max over lanes of the passes a lane needs instead of the sum
+// over candidates of the per-candidate maximum.
+// NS slots per lane walk NS candidates at once (NS x FB gathers in flight per
+// pass; the walk is bound by gather round trips, not by VALU).  Candidates
+// are handed to the slots in descending order; `best` is the smallest index
+// found stable so far, and a candidate above it is never started or is
+// dropped -- the answer, the first stable candidate in descending order, is
+// the reference's largest d != 0 with stability >= 0.
+// Preparation (wave 0, registers with static indices): the proj values are
+// sorted descending; the first stability term of candidate d is
+// 2 C - nnz with C = #{nonzero pj : |RN(pj - d)| <= fuse}.  RN(pj - d) is
+// monotone in pj, so in the sorted list that set is one contiguous run around
+// d: it is counted in a window of +-RI_WIN neighbours, and counted in full
+// (over the sorted list kept in LDS) when the run reaches the window's edge.
+// Distinct candidates are compacted into LDS (views holding the same d: one
+// evaluation).
+// ROWB (aw % FB == 0): a gather block's FB views lie in one camera row, so
+// their offsets are (kx + u, ky): one LDS read and one row projection per
+// block.  Disparities are finite (as for the lds/px forms; NaN inputs: the
+// generic k_remove_incons).
+constexpr int RI_WIN = 5;
+constexpr int8_t RI_OVER = -128;  // first term not yet counted (|term| <= 32)
+// reference-independent per-pixel candidate lists (see k_remove_incons_q)
+struct RiShared {
+  float sv[RI_MAXV][64];   // distinct candidates, descending
+  float srt[RI_MAXV][64];  // the sorted list (preparation only)
+  int8_t a[RI_MAXV][64];   // first stability term of each distinct candidate
+  int nd[64];              // distinct candidates per pixel
+};
+// wave 0 of the workgroup, lane = pixel
+__device__ __forceinline__ void ri_prep(RiShared& S, const float* __restrict__ proj, long P, long p, bool xin, int V,
+                                        float fuse, int lane) {
+  float sv[RI_MAXV];
+  int nnz = 0;
+#pragma unroll
+  for (int j = 0; j < RI_MAXV; j++) {
+    const float v = (xin && j < V) ? proj[P * j + p] : 0.0f;
+    nnz += v != 0;
+    sv[j] = v != 0 ? v : -INFINITY;  // non-candidates sort last
+  }
+  sort_desc<RI_MAXV>(sv);
+#pragma unroll
+  for (int j = 0; j < RI_MAXV; j++) S.srt[j][lane] = sv[j];
+  int nd = 0;
+#pragma unroll
+  for (int k = 0; k < RI_MAXV; k++) {
+    const float d = sv[k];
+    if (k < nnz && (k == 0 || d != sv[k > 0 ? k - 1 : 0])) {
+      int c = 0;
+#pragma unroll
+      for (int i = k - RI_WIN; i <= k + RI_WIN; i++)
+        if (i >= 0 && i < RI_MAXV) c += (i < nnz && fabsf(sv[i] - d) <= fuse) ? 1 : 0;
+      // the run reaches the window's edge.  (The empty asm keeps this
+      // compiler from dropping the whole preparation: with both edge tests
+      // feeding one boolean it deleted the loop at -O3, ROCm 7.2 clang.)
+      int ov = 0;
+      if (k - RI_WIN - 1 >= 0) ov |= fabsf(sv[k - RI_WIN - 1 >= 0 ? k - RI_WIN - 1 : 0] - d) <= fuse ? 1 : 0;
+      if (k + RI_WIN + 1 < RI_MAXV)
+        ov |= (k + RI_WIN + 1 < nnz && fabsf(sv[k + RI_WIN + 1 < RI_MAXV ? k + RI_WIN + 1 : 0] - d) <= fuse) ? 2 : 0;
+      asm volatile("" : "+v"(ov));
+      S.sv[nd][lane] = d;
+      S.a[nd][lane] = ov != 0 ? RI_OVER : (int8_t)(2 * c - nnz);
+      nd++;
+    }
+  }
+  // runs reaching the window's edge (marked RI_OVER): counted in full over
+  // the sorted list (each lane reads only its own column)
+  for (int q = 0; q < nd; q++) {
+    if (S.a[q][lane] != RI_OVER) continue;
+    const float d = S.sv[q][lane];
+    int c = 0;
+    for (int i = 0; i < nnz; i++) c += fabsf(S.srt[i][lane] - d) <= fuse ? 1 : 0;
+    S.a[q][lane] = (int8_t)(2 * c - nnz);
+  }
+  S.nd[lane] = nd;
+}
+
+template <int RG, int FB, int NS, bool ROWB>
+__global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __restrict__ proj,
+                                                             const float* __restrict__ full, int V, int W, int H,
+                                                             int aw, float bl, float fuse, int z0, int z1,
+                                                             float* __restrict__ out) {
+  __shared__ RiShared S;
+  __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int x = blockIdx.x * 64 + lane, y = blockIdx.y;
+  const bool xin = x < W;
+  const long P = (long)W * H, p = (long)y * W + (xin ? x : 0);
+  {
+    const int r = z0 + RG * blockIdx.z + wave;
+    if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the reference evaluates them
+      s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
+  }
+  if (wave == 0) ri_prep(S, proj, P, p, xin, V, fuse, lane);
+  __syncthreads();
+  const int r = z0 + RG * blockIdx.z + wave;
+  if (r >= z1 || !xin) return;  // after the only barrier
+  const float xf = (float)x, yf = (float)y;
+  const unsigned P4 = (unsigned)(P * 4);  // the launcher checks V * P * 4 < 2^31
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)full, 0, 0x7fffffff, 0x00020000);
+  const int nd = S.nd[lane];
+  int best = nd;  // smallest candidate index found stable (nd: none yet)
+  int nxt = 0;    // next candidate to hand to a slot
+  int k[NS], j[NS], st[NS];
+  unsigned jo[NS];  // j * P4: byte offset of view j
+  float d[NS], bd[NS];
+  auto take = [&](int s) {  // hand candidate nxt to slot s (k = nd: idle)
+    k[s] = nxt < best ? nxt : nd;
+    if (k[s] < nd) {
+      nxt++;
+      d[s] = S.sv[k[s]][lane];
+      st[s] = S.a[k[s]][lane];
+      bd[s] = bl * d[s];
+    }
+    j[s] = 0;
+    jo[s] = 0;
+  };
+#pragma unroll
+  for (int s = 0; s < NS; s++) take(s);
+  while (k[0] < best || (NS > 1 && k[NS > 1 ? 1 : 0] < best)) {
+    float dc[NS][FB];
+    bool in[NS][FB];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      const bool live = k[s] < best;
+      if (ROWB) {
+        const float2 o = s_off[wave][j[s]];
+        const int yy = (int)(yf - round_ha(bd[s] * o.y));
+        const bool yok = live && (unsigned)yy < (unsigned)H;
+        const unsigned ro = jo[s] + __umul24((unsigned)yy, (unsigned)W) * 4u;
+#pragma unroll
+        for (int u = 0; u < FB; u++) {
+          const int xx = (int)(xf - round_ha(d[s] * (o.x + (float)u)));
+          in[s][u] = yok && j[s] + u < V && (unsigned)xx < (unsigned)W;
+          // every lane issues its load (a skipped tap reads 0 past the buffer),
+          // so the pass's gathers are in flight together
+          const int off = in[s][u] ? (int)(ro + (unsigned)u * P4 + (unsigned)xx * 4u) : 0x7fffffff;
+          dc[s][u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < FB; u++) {
+          const float2 o = s_off[wave][min(j[s] + u, V - 1)];
+          const int xx = (int)(xf - round_ha(d[s] * o.x));
+          const int yy = (int)(yf - round_ha(bd[s] * o.y));
+          in[s][u] = live && j[s] + u < V && (unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H;
+          const int off =
+              in[s][u] ? (int)(jo[s] + (unsigned)u * P4 + (__umul24((unsigned)yy, (unsigned)W) + (unsigned)xx) * 4u) : 0x7fffffff;
+          dc[s][u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+#pragma unroll
+      for (int u = 0; u < FB; u++) {
+        const float ad = fabsf(dc[s][u] - d[s]);
+        st[s] += in[s][u] ? (ad < fuse ? 1 : 0) - (ad > fuse ? 1 : 0) : 0;
+      }
+      j[s] += FB;
+      jo[s] += FB * P4;
+    }
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      if (k[s] >= best) continue;
+      // each remaining view adds at most +1: a candidate is given up once
+      // stab >= 0 is out of reach (stab counts exactly: this only skips work)
+      const bool fin = j[s] >= V;
+      if (fin && st[s] >= 0) {
+        best = k[s];  // stable; every slot above it is dropped by the loop test
+        k[s] = nd;
+      } else if (fin || st[s] + (V - j[s]) < 0) {
+        take(s);
+      }
+    }
+  }
+  out[P * r + p] = best < nd ? S.sv[best][lane] : 0.0f;
+}
+
+// The same answer with the wave's work balanced over its lanes.  In
+// k_remove_incons_q a lane walks its own pixel's candidates, so a wave runs
+// as long as its slowest pixel (measured at C4: ~42 gather passes per wave
+// where a lane needs ~19 on average; the kernel is VALU-issue bound at
+// 0.8, most of it idle lanes' slots).  Here the wave's work items are the
+// (pixel, candidate) pairs of its 64 pixels, handed out in candidate-major
+// order -- every pixel's candidate 0, then every pixel's candidate 1, ... --
+// to whichever lanes are idle (ballot + mbcnt ranks, an LDS slot table).  A
+// lane walks its item's views in blocks of FB; a stable item lowers its
+// pixel's best index (LDS atomic min), and items above a pixel's best are
+// never handed out (or are dropped).  Each pixel's answer is its smallest
+// stable candidate index -- the first stable candidate in descending order,
+// as in k_remove_incons_q -- since every candidate below it was handed out
+// and proven unstable.  Measured at C4: 21.1 ms against k_remove_incons_q's
+// 18.1 (all 32 references with k_proj_inv): the hand-out rounds cost VALU/LDS
+// round trips, and lanes working other pixels' items spread a gather
+// instruction over more cache lines (the TA was already 75 % busy).  Kept as
+// an A/B option (MVS_FILTER_KERNEL=b).
+template <int RG, int FB, bool ROWB>
+__global__ __launch_bounds__(64 * RG) void k_remove_incons_b(const float* __restrict__ proj,
+                                                             const float* __restrict__ full, int V, int W, int H,
+                                                             int aw, float bl, float fuse, int z0, int z1,
+                                                             float* __restrict__ out) {
+  __shared__ RiShared S;
+  __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
+  __shared__ int s_best[RG][64];         // per wave: smallest candidate index found stable, per pixel
+  __shared__ int s_slot[RG][64];         // per wave: hand-out table
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int x0 = blockIdx.x * 64, y = blockIdx.y;
+  const bool xin = x0 + lane < W;
+  const long P = (long)W * H, prow = (long)y * W;
+  {
+    const int r = z0 + RG * blockIdx.z + wave;
+    if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the reference evaluates them
+      s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
+  }
+  if (wave == 0) ri_prep(S, proj, P, prow + (xin ? x0 + lane : 0), xin, V, fuse, lane);
+  __syncthreads();
+  const int r = z0 + RG * blockIdx.z + wave;
+  if (r >= z1) return;  // whole wave, after the only barrier
+  auto wsync = [] {     // this wave's LDS writes visible to its other lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  int* best = s_best[wave];
+  const int ndl = S.nd[lane];  // lane as pixel: its distinct candidates
+  best[lane] = ndl;            // none stable yet
+  wsync();
+  const float yf = (float)y;
+  const unsigned P4 = (unsigned)(P * 4);  // the launcher checks V * P * 4 < 2^31
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)full, 0, 0x7fffffff, 0x00020000);
+  // this lane's item: pixel ip, candidate ik, next view j (byte offset jo)
+  bool busy = false;
+  int ip = 0, ik = 0, j = 0, st = 0;
+  unsigned jo = 0;
+  float d = 0.0f, bd = 0.0f, xf = 0.0f;
+  int ck = 0;                // hand-out round: candidate index (wave-uniform)
+  unsigned long long taken = 0;  // pixels of round ck handed out (wave-uniform)
+  while (true) {
+    unsigned long long need = __builtin_amdgcn_ballot_w64(!busy);
+    while (need != 0 && ck < RI_MAXV) {
+      const int bl_ = __hip_atomic_load(&best[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const unsigned long long avail = __builtin_amdgcn_ballot_w64(ndl > ck && bl_ > ck) & ~taken;
+      if (avail == 0) {
+        ck++;
+        taken = 0;
+        continue;
+      }
+      const int ra = __builtin_amdgcn_mbcnt_hi((unsigned)(avail >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)avail, 0));
+      const int rn = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0));
+      const int na = __builtin_popcountll(avail), nn = __builtin_popcountll(need);
+      if ((avail >> lane) & 1ull) s_slot[wave][ra] = lane;
+      wsync();
+      if (!busy && rn < na) {
+        ip = s_slot[wave][rn];
+        ik = ck;
+        busy = true;
+        d = S.sv[ck][ip];
+        st = S.a[ck][ip];
+        bd = bl * d;
+        xf = (float)(x0 + ip);
+        j = 0;
+        jo = 0;
+      }
+      taken |= __builtin_amdgcn_ballot_w64(((avail >> lane) & 1ull) && ra < nn);
+      need = __builtin_amdgcn_ballot_w64(!busy);
+      wsync();  // the slot table is rewritten by the next round
+    }
+    if (__builtin_amdgcn_ballot_w64(busy) == 0) break;  // nothing in flight, nothing left
+    if (busy) {
+      float dc[FB];
+      bool in[FB];
+      if (ROWB) {
+        const float2 o = s_off[wave][j];
+        const int yy = (int)(yf - round_ha(bd * o.y));
+        const bool yok = (unsigned)yy < (unsigned)H;
+        const unsigned ro = jo + __umul24((unsigned)yy, (unsigned)W) * 4u;
+#pragma unroll
+        for (int u = 0; u < FB; u++) {
+          const int xx = (int)(xf - round_ha(d * (o.x + (float)u)));
+          in[u] = yok && j + u < V && (unsigned)xx < (unsigned)W;
+          const int off = in[u] ? (int)(ro + (unsigned)u * P4 + (unsigned)xx * 4u) : 0x7fffffff;
+          dc[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < FB; u++) {
+          const float2 o = s_off[wave][min(j + u, V - 1)];
+          const int xx = (int)(xf - round_ha(d * o.x));
+          const int yy = (int)(yf - round_ha(bd * o.y));
+          in[u] = j + u < V && (unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H;
+          const int off =
+              in[u] ? (int)(jo + (unsigned)u * P4 + (__umul24((unsigned)yy, (unsigned)W) + (unsigned)xx) * 4u) : 0x7fffffff;
+          dc[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < FB; u++) {
+        const float ad = fabsf(dc[u] - d);
+        st += in[u] ? (ad < fuse ? 1 : 0) - (ad > fuse ? 1 : 0) : 0;
+      }
+      j += FB;
+      jo += FB * P4;
+      const bool fin = j >= V;
+      if (fin && st >= 0) {
+        __hip_atomic_fetch_min(&best[ip], ik, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        busy = false;
+      } else if (fin || st + (V - j) < 0 ||
+                 __hip_atomic_load(&best[ip], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) < ik) {
+        busy = false;  // unstable, or a smaller candidate of the pixel is stable
+      }
+    }
+    wsync();
+  }
+  if (xin) {
+    const int b = best[lane];
+    out[P * r + prow + x0 + lane] = b < ndl ? S.sv[b][lane] : 0.0f;
+  }
+}
+
 }  // namespace
 
 int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
@@ -1132,22 +1466,72 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
                          out);
     else if (V <= 32 && (long)V * W * H * 4 < (1L << 31) &&
              !(getenv("MVS_FILTER_KERNEL") && std::string(getenv("MVS_FILTER_KERNEL")) == "px")) {
-      // shared-preparation form, 32-bit gather offsets (MVS_FILTER_KERNEL=px:
-      // the per-pixel form below)
+      // 32-bit gather offsets.  Default: one work queue per lane
+      // (k_remove_incons_q, MVS_FILTER_NS candidates at once);
+      // MVS_FILTER_KERNEL=b: the wave's (pixel, candidate) items balanced over
+      // its lanes, =lds: the lock-step walk (MVS_FILTER_CP candidates
+      // together), =px: the per-pixel form below.  MVS_FILTER_FB (read per
+      // call): views per gather block.  Measured at C4, all 32 references
+      // with k_proj_inv (scripts/bench_filter.py): q 18.1 ms (NS 2, FB 2),
+      // b 21.1 ms (FB 2), lds 27.9 ms.
       constexpr int RG = 4;
       const dim3 gl((W + 63) / 64, H, (z1 - z0 + RG - 1) / RG);
-      // MVS_FILTER_CP: candidates evaluated together (1 | 2 | 3; A/B, read per call)
-      const char* cp = getenv("MVS_FILTER_CP");
-      const int ncp = cp ? atoi(cp) : 2;
-      if (ncp == 1)
-        hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 1>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, fuse,
-                           z0, z1, out);
-      else if (ncp == 3)
-        hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 3>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, fuse,
-                           z0, z1, out);
-      else
-        hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 2>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, fuse,
-                           z0, z1, out);
+      const char* fk = getenv("MVS_FILTER_KERNEL");
+      if (fk && std::string(fk) == "lds") {
+        const char* cp = getenv("MVS_FILTER_CP");
+        const int ncp = cp ? atoi(cp) : 2;
+        if (ncp == 1)
+          hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 1>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
+                             fuse, z0, z1, out);
+        else if (ncp == 3)
+          hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 3>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
+                             fuse, z0, z1, out);
+        else
+          hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 2>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
+                             fuse, z0, z1, out);
+      } else if (fk && std::string(fk) == "b") {
+        const char* fb = getenv("MVS_FILTER_FB");
+        const int nfb = fb ? atoi(fb) : 4;
+#define MVS_RIB(FBV)                                                                                              \
+  if (aw % FBV == 0)                                                                                              \
+    hipLaunchKernelGGL((k_remove_incons_b<RG, FBV, true>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,  \
+                       fuse, z0, z1, out);                                                                        \
+  else                                                                                                            \
+    hipLaunchKernelGGL((k_remove_incons_b<RG, FBV, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, \
+                       fuse, z0, z1, out);
+        if (nfb == 2) {
+          MVS_RIB(2)
+        } else if (nfb == 8) {
+          MVS_RIB(8)
+        } else {
+          MVS_RIB(4)
+        }
+#undef MVS_RIB
+      } else {
+        const char* fb = getenv("MVS_FILTER_FB");
+        const int nfb = fb ? atoi(fb) : 2;
+#define MVS_RIQ(FBV, NSV)                                                                                         \
+  if (aw % FBV == 0)                                                                                              \
+    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, \
+                       bl, fuse, z0, z1, out);                                                                    \
+  else                                                                                                            \
+    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H,    \
+                       aw, bl, fuse, z0, z1, out);
+        const char* ns = getenv("MVS_FILTER_NS");  // candidate slots per lane (1 | 2)
+        const int nns = ns ? atoi(ns) : 2;
+        if (nns == 1) {
+          if (nfb == 4) {
+            MVS_RIQ(4, 1)
+          } else {
+            MVS_RIQ(2, 1)
+          }
+        } else if (nfb == 4) {
+          MVS_RIQ(4, 2)
+        } else {
+          MVS_RIQ(2, 2)
+        }
+#undef MVS_RIQ
+      }
     } else if (V <= 32) {
       // MVS_FILTER_FB: views per gather block (A/B; read per call).  Measured at
       // C4 (scripts/bench_filter.py): blocks of 8 gathers 54 ms for all 32

@@ -297,6 +297,31 @@ def test_filter_many_views(engine, aw, ah):
     assert_bits(out.cpu().numpy(), oout, "filter output")
 
 
+@pytest.mark.parametrize("kern,fb,ns", [("b", 2, 0), ("b", 4, 0), ("b", 8, 0), ("q", 2, 2), ("q", 4, 2), ("q", 2, 1),
+                                         ("q", 4, 1), ("lds", 4, 0), ("px", 4, 0), ("px", 2, 0)])
+@pytest.mark.parametrize("aw,ah", [(8, 4), (6, 5), (5, 5)])
+def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns):
+    # every removal kernel for 16 < V <= 32, forced per call (MVS_FILTER_KERNEL /
+    # _FB / _NS are read at each launch): the wave-balanced walk and the
+    # per-lane queue walk (1 or 2 candidate slots), each with row-shared
+    # (aw % FB == 0) and per-view offsets, the lock-step walk and the
+    # per-pixel form.  Near-equal candidates in long runs reach the queue
+    # kernel's full-count fallback of the first stability term.
+    V, H, W = aw * ah, 20, 72
+    rng = np.random.default_rng(aw * 100 + ah * 7 + fb)
+    base = rng.integers(2, 12, size=(V, 1, 1)).astype(np.float32)
+    disp = base + rng.choice(np.float32([0.0, 0.25, 0.5, 1.0, 1.5, 6.0]), size=(V, H, W))
+    disp[:, :4] = 5.0 + rng.choice(np.float32([0.0, 0.5]), size=(V, 4, W))  # long runs within fuse
+    disp[rng.random(disp.shape) < 0.1] = 0.0
+    monkeypatch.setenv("MVS_FILTER_KERNEL", kern)
+    monkeypatch.setenv("MVS_FILTER_FB", str(fb))
+    monkeypatch.setenv("MVS_FILTER_NS", str(ns))
+    proj, out = engine.filter(dev(disp), aw, 1.0359, 1.0)
+    oproj, oout = orc.filt(disp, aw, 1.0359, 1.0)
+    assert_bits(proj.cpu().numpy(), oproj, "filter projection")
+    assert_bits(out.cpu().numpy(), oout, f"filter output ({kern}, FB {fb})")
+
+
 def test_determinism(engine):
     c = CASES["c5x1_s32"]
     b = build(c)

@@ -337,3 +337,21 @@ def test_slic_edge_modes(S):
     assert np.array_equal(sp2[..., :6], moved[..., :6])
     assert (moved[..., 1:3] != init[..., 1:3]).any()
     assert np.array_equal(lb2, orc.assign(lab0, moved, S))
+
+
+def test_round_half_away_identity():
+    """k_remove_incons_q's round_ha: roundf(v) == truncf(v + copysignf(0.49999997f, v))
+    for every float.  Exhaustive over the positive floats below 2^23 (above, every
+    float is an integer and both sides return v; negatives are symmetric)."""
+    c = np.float32(np.frombuffer(np.uint32(0x3EFFFFFF).tobytes(), np.float32)[0])
+    top = int(np.frombuffer(np.float32(2.0 ** 23).tobytes(), np.uint32)[0])
+    step = 1 << 25
+    for lo in range(0, top, step):
+        v = np.arange(lo, min(lo + step, top), dtype=np.uint32).view(np.float32)
+        t = np.trunc(v + c)
+        r = np.trunc(v)
+        r = r + (v - r >= np.float32(0.5)).astype(np.float32)  # roundf: half away from zero
+        assert np.array_equal(t, r), lo
+    big = np.float32([2.0 ** 23, 2.0 ** 23 + 1, 2.0 ** 24 + 2, 3.0e38, np.inf])
+    assert np.array_equal(np.trunc(big + c), big)
+    assert np.array_equal(np.trunc(-big - c), -big)

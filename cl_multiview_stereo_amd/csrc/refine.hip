@@ -695,22 +695,47 @@ __global__ void k_spixl_to_image(const float* __restrict__ spixl, const uint32_t
 }
 
 // ---- cross-view filter -------------------------------------------------------
-__global__ void k_proj_inv(const float* __restrict__ full, int V, int W, int H, int aw, float bl, int z0,
-                           float* __restrict__ proj) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
+__device__ __forceinline__ float round_ha(float v);
+// Filter grid orders.  RM = false: (x tiles, rows, reference groups), so a
+// reference group streams the whole disparity stack before the next one
+// starts.  RM = true: (x tiles x reference groups, rows): every reference of
+// a row band is in flight together, sharing the views' rows they gather
+// around in L2.  Measured at C4 for k_remove_incons_q: 14.2 (RM) vs 14.6 ms.
+struct FGrid {
+  int xb, y, g;
+};
+template <bool RM>
+__device__ __forceinline__ FGrid fgrid(int tiles_x) {
+  if (RM) return {(int)blockIdx.x % tiles_x, (int)blockIdx.y, (int)blockIdx.x / tiles_x};
+  return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+}
+// project_to_reference_inv: per (reference r, pixel) the running maximum md
+// over the other views i of full[i] at the pixel projected with md itself
+// (clcode.cl:1995-2034) -- a chain of dependent gathers, one thread per
+// (reference, pixel).  Per-view buffer resources (scalar), so an out-of-image
+// tap reads 0 through a load past the end and is skipped, as in the
+// reference, without a branch.  Measured (C4, 32 references): 3.4 ms;
+// issuing blocks of 4 / 8 views' gathers speculatively with the block's
+// starting maximum (re-gathered once it moves) 4.1 / 4.4 ms, and a
+// row-major grid (every reference of a row in flight together) 6.0 ms.
+__global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full, int V, int W, int H, int aw,
+                                                  float bl, int z0, float* __restrict__ proj) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
   if (x >= W) return;
-  long P = (long)W * H, p = (long)y * W + x;
-  int crx = r % aw, cry = r / aw;
+  const long P = (long)W * H, p = (long)y * W + x;
+  const int crx = r % aw, cry = r / aw;
+  const float xf = (float)x, yf = (float)y;
   float md = full[P * r + p];
   for (int i = 0; i < V; i++) {
     if (i == r) continue;
-    int cx = i % aw, cy = i / aw;
-    int xp = (int)((float)x - roundf(md * (float)(crx - cx)));
-    int yp = (int)((float)y - roundf((bl * md) * (float)(cry - cy)));
-    if (xp >= 0 && yp >= 0 && xp < W && yp < H) {
-      float cd = full[P * i + (long)W * yp + xp];
-      if (md < cd) md = cd;
-    }
+    const int cx = i % aw, cy = i / aw;
+    const int xp = (int)(xf - round_ha(md * (float)(crx - cx)));
+    const int yp = (int)(yf - round_ha((bl * md) * (float)(cry - cy)));
+    const bool in = (unsigned)xp < (unsigned)W && (unsigned)yp < (unsigned)H;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(full + P * i), 0, 0x7fffffff, 0x00020000);
+    const int off = in ? (int)((unsigned)yp * (unsigned)W + (unsigned)xp) * 4 : 0x7fffffff;
+    const float cd = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+    if (in && md < cd) md = cd;
   }
   proj[P * r + p] = md;
 }
@@ -1155,7 +1180,7 @@ __device__ __forceinline__ void ri_prep(RiShared& S, const float* __restrict__ p
   S.nd[lane] = nd;
 }
 
-template <int RG, int FB, int NS, bool ROWB>
+template <int RG, int FB, int NS, bool ROWB, bool RM>
 __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __restrict__ proj,
                                                              const float* __restrict__ full, int V, int W, int H,
                                                              int aw, float bl, float fuse, int z0, int z1,
@@ -1163,17 +1188,18 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
   __shared__ RiShared S;
   __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int x = blockIdx.x * 64 + lane, y = blockIdx.y;
+  const FGrid fg = fgrid<RM>((W + 63) / 64);
+  const int x = fg.xb * 64 + lane, y = fg.y;
   const bool xin = x < W;
   const long P = (long)W * H, p = (long)y * W + (xin ? x : 0);
   {
-    const int r = z0 + RG * blockIdx.z + wave;
+    const int r = z0 + RG * fg.g + wave;
     if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the reference evaluates them
       s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
   }
   if (wave == 0) ri_prep(S, proj, P, p, xin, V, fuse, lane);
   __syncthreads();
-  const int r = z0 + RG * blockIdx.z + wave;
+  const int r = z0 + RG * fg.g + wave;
   if (r >= z1 || !xin) return;  // after the only barrier
   const float xf = (float)x, yf = (float)y;
   const unsigned P4 = (unsigned)(P * 4);  // the launcher checks V * P * 4 < 2^31
@@ -1511,12 +1537,20 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
         const char* fb = getenv("MVS_FILTER_FB");
         const int nfb = fb ? atoi(fb) : 2;
 #define MVS_RIQ(FBV, NSV)                                                                                         \
-  if (aw % FBV == 0)                                                                                              \
-    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, \
-                       bl, fuse, z0, z1, out);                                                                    \
+  if (aw % FBV == 0 && rmo)                                                                                       \
+    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true, true>), glr, dim3(64 * RG), 0, s, proj, full, V, W, \
+                       H, aw, bl, fuse, z0, z1, out);                                                             \
+  else if (aw % FBV == 0)                                                                                         \
+    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, \
+                       H, aw, bl, fuse, z0, z1, out);                                                             \
+  else if (rmo)                                                                                                   \
+    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false, true>), glr, dim3(64 * RG), 0, s, proj, full, V,   \
+                       W, H, aw, bl, fuse, z0, z1, out);                                                          \
   else                                                                                                            \
-    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H,    \
-                       aw, bl, fuse, z0, z1, out);
+    hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false, false>), gl, dim3(64 * RG), 0, s, proj, full, V,   \
+                       W, H, aw, bl, fuse, z0, z1, out);
+        const bool rmo = !(getenv("MVS_FILTER_ORDER") && std::string(getenv("MVS_FILTER_ORDER")) == "ref");
+        const dim3 glr(((W + 63) / 64) * ((z1 - z0 + RG - 1) / RG), H);
         const char* ns = getenv("MVS_FILTER_NS");  // candidate slots per lane (1 | 2)
         const int nns = ns ? atoi(ns) : 2;
         if (nns == 1) {

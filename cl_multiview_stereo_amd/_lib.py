@@ -19,7 +19,7 @@ EXPORTS = [
     "mvs_box_stats_d", "mvs_ncc_volume_d", "mvs_wta_d", "mvs_ncc_wta_d", "mvs_flatness_d", "mvs_init_state_d",
     "mvs_propagate_d", "mvs_spixl_to_image_d", "mvs_refine_d", "mvs_filter_d",
     "mvs_box_stats_range_d", "mvs_set_ncc_variant", "mvs_ncc_last_variant", "mvs_init_state_range_d",
-    "mvs_proj_inv_d", "mvs_remove_inconsistency_d",
+    "mvs_proj_inv_d", "mvs_remove_inconsistency_d", "mvs_proj_inv_rows_d", "mvs_remove_inconsistency_rows_d",
     "mvs_do_super_pixel_seg", "mvs_do_initial_depth_estimation", "mvs_do_refinement", "mvs_do_consistency_filter",
 ]
 

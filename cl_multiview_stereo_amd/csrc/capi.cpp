@@ -430,7 +430,15 @@ int mvs_proj_inv_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ra
                    float* proj, int z0, int z1) {
   if (!c || !disp_full || !proj || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V || z0 > z1)
     return mvs::arg_fail("mvs_proj_inv_d: bad arguments");
-  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1);
+  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1, 0, H);
+}
+
+int mvs_proj_inv_rows_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, const float* disp_full,
+                        float* proj, int z0, int z1, int y0, int y1) {
+  if (!c || !disp_full || !proj || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V || z0 > z1 ||
+      y0 < 0 || y1 > H || y0 > y1)
+    return mvs::arg_fail("mvs_proj_inv_rows_d: bad arguments");
+  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1, y0, y1);
 }
 
 int mvs_remove_inconsistency_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, float fuse,
@@ -439,7 +447,17 @@ int mvs_remove_inconsistency_d(mvs_ctx* c, int V, int W, int H, int array_width,
       z0 > z1)
     return mvs::arg_fail("mvs_remove_inconsistency_d: bad arguments");
   return mvs::launch_remove_incons(c->stream, V, W, H, array_width, bl_ratio, (float)(0.5 * (double)fuse), disp_full,
-                                   proj, out, z0, z1);
+                                   proj, out, z0, z1, 0, H, false);
+}
+
+int mvs_remove_inconsistency_rows_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, float fuse,
+                                    const float* disp_full, const float* proj, int proj_band, float* out, int z0,
+                                    int z1, int y0, int y1) {
+  if (!c || !disp_full || (!proj && y1 > y0) || !out || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V ||
+      z0 > z1 || y0 < 0 || y1 > H || y0 > y1)
+    return mvs::arg_fail("mvs_remove_inconsistency_rows_d: bad arguments");
+  return mvs::launch_remove_incons(c->stream, V, W, H, array_width, bl_ratio, (float)(0.5 * (double)fuse), disp_full,
+                                   proj, out, z0, z1, y0, y1, proj_band != 0);
 }
 
 // ---- host-pointer API (reference stage methods) ----------------------------------

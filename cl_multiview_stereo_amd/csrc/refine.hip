@@ -705,9 +705,9 @@ struct FGrid {
   int xb, y, g;
 };
 template <bool RM>
-__device__ __forceinline__ FGrid fgrid(int tiles_x) {
-  if (RM) return {(int)blockIdx.x % tiles_x, (int)blockIdx.y, (int)blockIdx.x / tiles_x};
-  return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+__device__ __forceinline__ FGrid fgrid(int tiles_x, int y0) {
+  if (RM) return {(int)blockIdx.x % tiles_x, y0 + (int)blockIdx.y, (int)blockIdx.x / tiles_x};
+  return {(int)blockIdx.x, y0 + (int)blockIdx.y, (int)blockIdx.z};
 }
 // project_to_reference_inv: per (reference r, pixel) the running maximum md
 // over the other views i of full[i] at the pixel projected with md itself
@@ -719,8 +719,8 @@ __device__ __forceinline__ FGrid fgrid(int tiles_x) {
 // starting maximum (re-gathered once it moves) 4.1 / 4.4 ms, and a
 // row-major grid (every reference of a row in flight together) 6.0 ms.
 __global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full, int V, int W, int H, int aw,
-                                                  float bl, int z0, float* __restrict__ proj) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
+                                                  float bl, int z0, float* __restrict__ proj, int ya) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = ya + blockIdx.y, r = z0 + blockIdx.z;
   if (x >= W) return;
   const long P = (long)W * H, p = (long)y * W + x;
   const int crx = r % aw, cry = r / aw;
@@ -739,20 +739,58 @@ __global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full
   }
   proj[P * r + p] = md;
 }
+// The same chain for NC pixels per thread (rows y0 .. y0 + NC - 1 of one
+// column), the NC chains interleaved view by view: per view the NC gathers are
+// issued together, so a wave keeps NC independent loads in flight where
+// k_proj_inv keeps one (k_proj_inv is bound by the chain's gather latency,
+// not by the TA or L2: ~0.9 us per gather at full occupancy).
+template <int NC>
+__global__ __launch_bounds__(256) void k_proj_inv_mc(const float* __restrict__ full, int V, int W, int H, int aw,
+                                                     float bl, int z0, float* __restrict__ proj, int ya, int yb) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y0 = ya + blockIdx.y * NC, r = z0 + blockIdx.z;
+  if (x >= W) return;
+  const long P = (long)W * H;
+  const int crx = r % aw, cry = r / aw;
+  const float xf = (float)x;
+  float md[NC];
+#pragma unroll
+  for (int c = 0; c < NC; c++) md[c] = y0 + c < yb ? full[P * r + (long)(y0 + c) * W + x] : 0.0f;
+  for (int i = 0; i < V; i++) {
+    if (i == r) continue;
+    const float fdx = (float)(crx - i % aw), fdy = (float)(cry - i / aw);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(full + P * i), 0, 0x7fffffff, 0x00020000);
+    bool in[NC];
+    float cd[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      const int xp = (int)(xf - round_ha(md[c] * fdx));
+      const int yp = (int)((float)(y0 + c) - round_ha((bl * md[c]) * fdy));
+      in[c] = (unsigned)xp < (unsigned)W && (unsigned)yp < (unsigned)H;
+      const int off = in[c] ? (int)((unsigned)yp * (unsigned)W + (unsigned)xp) * 4 : 0x7fffffff;
+      cd[c] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+      if (in[c] && md[c] < cd[c]) md[c] = cd[c];
+  }
+#pragma unroll
+  for (int c = 0; c < NC; c++)
+    if (y0 + c < yb) proj[P * r + (long)(y0 + c) * W + x] = md[c];
+}
 
 __global__ void k_remove_incons(const float* __restrict__ proj, const float* __restrict__ full, int V, int W, int H,
-                                int aw, float bl, float fuse, int z0, float* __restrict__ out) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
+                                int aw, float bl, float fuse, int z0, float* __restrict__ out, int y0, long PP) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = y0 + blockIdx.y, r = z0 + blockIdx.z;
   if (x >= W) return;
   long P = (long)W * H, p = (long)y * W + x;
   int crx = r % aw, cry = r / aw;
   float dest = 0.0f;
   for (int i = 0; i < V; i++) {
-    float d = proj[P * i + p];
+    float d = proj[PP * i + p];
     if (d != 0) {
       float stab = 0.0f;
       for (int j = 0; j < V; j++) {
-        float dc = proj[P * j + p];
+        float dc = proj[PP * j + p];
         if (dc != 0) {
           float diff = dc - d;
           if (fabsf(diff) > fuse) stab = stab - 1.0f;
@@ -786,8 +824,8 @@ __global__ void k_remove_incons(const float* __restrict__ proj, const float* __r
 template <int MAXV>
 __global__ __launch_bounds__(256) void k_remove_incons_sel(const float* __restrict__ proj, const float* __restrict__ full,
                                                            int V, int W, int H, int aw, float bl, float fuse, int z0,
-                                                           float* __restrict__ out) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, r = z0 + blockIdx.z;
+                                                           float* __restrict__ out, int y0, long PP) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = y0 + blockIdx.y, r = z0 + blockIdx.z;
   if (x >= W) return;
   long P = (long)W * H, p = (long)y * W + x;
   int crx = r % aw, cry = r / aw;
@@ -795,7 +833,7 @@ __global__ __launch_bounds__(256) void k_remove_incons_sel(const float* __restri
   unsigned long long live = 0ull;  // candidates not yet tried: d != 0
 #pragma unroll
   for (int i = 0; i < MAXV; i++) {
-    pv[i] = i < V ? proj[P * i + p] : 0.0f;
+    pv[i] = i < V ? proj[PP * i + p] : 0.0f;
     if (pv[i] != 0) live |= 1ull << i;
   }
   float dest = 0.0f;
@@ -880,14 +918,14 @@ __device__ __forceinline__ void sort_desc(float (&v)[N]) {
 template <int MAXV, int FB>  // FB: views per gather block (gathers in flight together)
 __global__ __launch_bounds__(256) void k_remove_incons_px(const float* __restrict__ proj, const float* __restrict__ full,
                                                           int V, int W, int H, int aw, float bl, float fuse, int z0,
-                                                          int z1, float* __restrict__ out) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+                                                          int z1, float* __restrict__ out, int y0, long PP) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = y0 + blockIdx.y;
   if (x >= W) return;
   const long P = (long)W * H, p = (long)y * W + x;
   float pv[MAXV], sv[MAXV];
 #pragma unroll
   for (int i = 0; i < MAXV; i++) {
-    pv[i] = i < V ? proj[P * i + p] : 0.0f;
+    pv[i] = i < V ? proj[PP * i + p] : 0.0f;
     sv[i] = pv[i] != 0 ? pv[i] : -INFINITY;  // non-candidates sort last
   }
   sort_desc<MAXV>(sv);
@@ -959,16 +997,16 @@ template <int RG, int FB, int CP>
 __global__ __launch_bounds__(64 * RG) void k_remove_incons_lds(const float* __restrict__ proj,
                                                                const float* __restrict__ full, int V, int W, int H,
                                                                int aw, float bl, float fuse, int z0, int z1,
-                                                               float* __restrict__ out) {
+                                                               float* __restrict__ out, int y0, long PP) {
   __shared__ float s_pv[RI_MAXV][64];  // proj values at the pixel, per view
   __shared__ float s_sv[RI_MAXV][64];  // candidates sorted descending (-inf: none)
   __shared__ float s_a[RI_MAXV][64];   // first stability term of each sorted candidate
   __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int x = blockIdx.x * 64 + lane, y = blockIdx.y;
+  const int x = blockIdx.x * 64 + lane, y = y0 + blockIdx.y;
   const bool xin = x < W;
   const long P = (long)W * H, p = (long)y * W + (xin ? x : 0);
-  for (int j = wave; j < RI_MAXV; j += RG) s_pv[j][lane] = (xin && j < V) ? proj[P * j + p] : 0.0f;
+  for (int j = wave; j < RI_MAXV; j += RG) s_pv[j][lane] = (xin && j < V) ? proj[PP * j + p] : 0.0f;
   {
     const int r = z0 + RG * blockIdx.z + wave;
     if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the walk evaluates them
@@ -1184,11 +1222,11 @@ template <int RG, int FB, int NS, bool ROWB, bool RM>
 __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __restrict__ proj,
                                                              const float* __restrict__ full, int V, int W, int H,
                                                              int aw, float bl, float fuse, int z0, int z1,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, int y0, long PP) {
   __shared__ RiShared S;
   __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const FGrid fg = fgrid<RM>((W + 63) / 64);
+  const FGrid fg = fgrid<RM>((W + 63) / 64, y0);
   const int x = fg.xb * 64 + lane, y = fg.y;
   const bool xin = x < W;
   const long P = (long)W * H, p = (long)y * W + (xin ? x : 0);
@@ -1197,7 +1235,7 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
     if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the reference evaluates them
       s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
   }
-  if (wave == 0) ri_prep(S, proj, P, p, xin, V, fuse, lane);
+  if (wave == 0) ri_prep(S, proj, PP, p, xin, V, fuse, lane);
   __syncthreads();
   const int r = z0 + RG * fg.g + wave;
   if (r >= z1 || !xin) return;  // after the only barrier
@@ -1305,13 +1343,13 @@ template <int RG, int FB, bool ROWB>
 __global__ __launch_bounds__(64 * RG) void k_remove_incons_b(const float* __restrict__ proj,
                                                              const float* __restrict__ full, int V, int W, int H,
                                                              int aw, float bl, float fuse, int z0, int z1,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, int y0, long PP) {
   __shared__ RiShared S;
   __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
   __shared__ int s_best[RG][64];         // per wave: smallest candidate index found stable, per pixel
   __shared__ int s_slot[RG][64];         // per wave: hand-out table
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int x0 = blockIdx.x * 64, y = blockIdx.y;
+  const int x0 = blockIdx.x * 64, y = y0 + blockIdx.y;
   const bool xin = x0 + lane < W;
   const long P = (long)W * H, prow = (long)y * W;
   {
@@ -1319,7 +1357,7 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_b(const float* __rest
     if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the reference evaluates them
       s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
   }
-  if (wave == 0) ri_prep(S, proj, P, prow + (xin ? x0 + lane : 0), xin, V, fuse, lane);
+  if (wave == 0) ri_prep(S, proj, PP, prow + (xin ? x0 + lane : 0), xin, V, fuse, lane);
   __syncthreads();
   const int r = z0 + RG * blockIdx.z + wave;
   if (r >= z1) return;  // whole wave, after the only barrier
@@ -1468,10 +1506,24 @@ int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float
 
 // project_to_reference_inv for reference views [z0, z1): proj slices z0..z1-1
 int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const float* full, float* proj, int z0,
-                    int z1) {
-  if (z1 <= z0) return 0;
-  hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, H, z1 - z0), dim3(256), 0, s, full, V, W, H, aw, bl, z0,
-                     proj);
+                    int z1, int ya, int yb) {
+  const int NR = yb - ya;  // rows [ya, yb) (the caller checks 0 <= ya <= yb <= H)
+  if (z1 <= z0 || NR <= 0) return 0;
+  // MVS_PROJ_NC (read per call): pixels (rows) per thread, 1 = k_proj_inv
+  const char* nce = getenv("MVS_PROJ_NC");
+  const int nc = nce ? atoi(nce) : 1;
+  if (nc == 2)
+    hipLaunchKernelGGL(k_proj_inv_mc<2>, dim3((W + 255) / 256, (NR + 1) / 2, z1 - z0), dim3(256), 0, s, full, V, W, H,
+                       aw, bl, z0, proj, ya, yb);
+  else if (nc == 4)
+    hipLaunchKernelGGL(k_proj_inv_mc<4>, dim3((W + 255) / 256, (NR + 3) / 4, z1 - z0), dim3(256), 0, s, full, V, W, H,
+                       aw, bl, z0, proj, ya, yb);
+  else if (nc == 8)
+    hipLaunchKernelGGL(k_proj_inv_mc<8>, dim3((W + 255) / 256, (NR + 7) / 8, z1 - z0), dim3(256), 0, s, full, V, W, H,
+                       aw, bl, z0, proj, ya, yb);
+  else
+    hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, NR, z1 - z0), dim3(256), 0, s, full, V, W, H, aw, bl, z0,
+                       proj, ya);
   MVS_LAUNCH_CHECK("k_proj_inv");
   return 0;
 }
@@ -1479,17 +1531,22 @@ int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const 
 // remove_view_inconsistency for reference views [z0, z1): reads every proj
 // slice (all V must be filled) and the full disparity stack
 int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
-                         const float* proj, float* out, int z0, int z1) {
-  if (z1 > z0) {
-    const dim3 g((W + 255) / 256, H, z1 - z0);
-    const dim3 gp((W + 255) / 256, H);
+                         const float* proj, float* out, int z0, int z1, int ya, int yb, bool band) {
+  const int NR = yb - ya;  // rows [ya, yb) only (the caller checks 0 <= ya <= yb <= H)
+  // band: proj holds rows [ya, yb) only, as [V][yb - ya][W] (the kernels index
+  // proj[PP * view + y * W + x], so the band's base moves up by ya rows)
+  const long PP = band ? (long)NR * W : (long)W * H;
+  if (band) proj -= (long)ya * W;
+  if (z1 > z0 && NR > 0) {
+    const dim3 g((W + 255) / 256, NR, z1 - z0);
+    const dim3 gp((W + 255) / 256, NR);
     // few views: one thread per (reference, pixel) keeps more threads in flight
     // (measured at V = 5: 350 vs 395 us); many views: one thread per pixel
     if (V <= 8)
-      hipLaunchKernelGGL(k_remove_incons_sel<8>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
+      hipLaunchKernelGGL(k_remove_incons_sel<8>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out, ya, PP);
     else if (V <= 16)
       hipLaunchKernelGGL((k_remove_incons_px<16, 8>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1,
-                         out);
+                         out, ya, PP);
     else if (V <= 32 && (long)V * W * H * 4 < (1L << 31) &&
              !(getenv("MVS_FILTER_KERNEL") && std::string(getenv("MVS_FILTER_KERNEL")) == "px")) {
       // 32-bit gather offsets.  Default: one work queue per lane
@@ -1501,30 +1558,30 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
       // with k_proj_inv (scripts/bench_filter.py): q 18.1 ms (NS 2, FB 2),
       // b 21.1 ms (FB 2), lds 27.9 ms.
       constexpr int RG = 4;
-      const dim3 gl((W + 63) / 64, H, (z1 - z0 + RG - 1) / RG);
+      const dim3 gl((W + 63) / 64, NR, (z1 - z0 + RG - 1) / RG);
       const char* fk = getenv("MVS_FILTER_KERNEL");
       if (fk && std::string(fk) == "lds") {
         const char* cp = getenv("MVS_FILTER_CP");
         const int ncp = cp ? atoi(cp) : 2;
         if (ncp == 1)
           hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 1>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
-                             fuse, z0, z1, out);
+                             fuse, z0, z1, out, ya, PP);
         else if (ncp == 3)
           hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 3>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
-                             fuse, z0, z1, out);
+                             fuse, z0, z1, out, ya, PP);
         else
           hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 2>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
-                             fuse, z0, z1, out);
+                             fuse, z0, z1, out, ya, PP);
       } else if (fk && std::string(fk) == "b") {
         const char* fb = getenv("MVS_FILTER_FB");
         const int nfb = fb ? atoi(fb) : 4;
 #define MVS_RIB(FBV)                                                                                              \
   if (aw % FBV == 0)                                                                                              \
     hipLaunchKernelGGL((k_remove_incons_b<RG, FBV, true>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,  \
-                       fuse, z0, z1, out);                                                                        \
+                       fuse, z0, z1, out, ya, PP);                                                                        \
   else                                                                                                            \
     hipLaunchKernelGGL((k_remove_incons_b<RG, FBV, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, \
-                       fuse, z0, z1, out);
+                       fuse, z0, z1, out, ya, PP);
         if (nfb == 2) {
           MVS_RIB(2)
         } else if (nfb == 8) {
@@ -1539,18 +1596,18 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
 #define MVS_RIQ(FBV, NSV)                                                                                         \
   if (aw % FBV == 0 && rmo)                                                                                       \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true, true>), glr, dim3(64 * RG), 0, s, proj, full, V, W, \
-                       H, aw, bl, fuse, z0, z1, out);                                                             \
+                       H, aw, bl, fuse, z0, z1, out, ya, PP);                                                             \
   else if (aw % FBV == 0)                                                                                         \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, \
-                       H, aw, bl, fuse, z0, z1, out);                                                             \
+                       H, aw, bl, fuse, z0, z1, out, ya, PP);                                                             \
   else if (rmo)                                                                                                   \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false, true>), glr, dim3(64 * RG), 0, s, proj, full, V,   \
-                       W, H, aw, bl, fuse, z0, z1, out);                                                          \
+                       W, H, aw, bl, fuse, z0, z1, out, ya, PP);                                                          \
   else                                                                                                            \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false, false>), gl, dim3(64 * RG), 0, s, proj, full, V,   \
-                       W, H, aw, bl, fuse, z0, z1, out);
+                       W, H, aw, bl, fuse, z0, z1, out, ya, PP);
         const bool rmo = !(getenv("MVS_FILTER_ORDER") && std::string(getenv("MVS_FILTER_ORDER")) == "ref");
-        const dim3 glr(((W + 63) / 64) * ((z1 - z0 + RG - 1) / RG), H);
+        const dim3 glr(((W + 63) / 64) * ((z1 - z0 + RG - 1) / RG), NR);
         const char* ns = getenv("MVS_FILTER_NS");  // candidate slots per lane (1 | 2)
         const int nns = ns ? atoi(ns) : 2;
         if (nns == 1) {
@@ -1575,18 +1632,18 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
       const int nfb = fb ? atoi(fb) : 4;
       if (nfb == 4)
         hipLaunchKernelGGL((k_remove_incons_px<32, 4>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0,
-                           z1, out);
+                           z1, out, ya, PP);
       else if (nfb == 2)
         hipLaunchKernelGGL((k_remove_incons_px<32, 2>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0,
-                           z1, out);
+                           z1, out, ya, PP);
       else
         hipLaunchKernelGGL((k_remove_incons_px<32, 8>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0,
-                           z1, out);
+                           z1, out, ya, PP);
     }
     else if (V <= 64)
-      hipLaunchKernelGGL(k_remove_incons_sel<64>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
+      hipLaunchKernelGGL(k_remove_incons_sel<64>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out, ya, PP);
     else
-      hipLaunchKernelGGL(k_remove_incons, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out);
+      hipLaunchKernelGGL(k_remove_incons, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out, ya, PP);
     MVS_LAUNCH_CHECK("k_remove_incons");
   }
   return 0;
@@ -1595,9 +1652,9 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
 // pinned order: every projection, then the removal
 int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
                   float* proj, float* out, int z0, int z1) {
-  int rc = launch_proj_inv(s, V, W, H, aw, bl, full, proj, 0, V);
+  int rc = launch_proj_inv(s, V, W, H, aw, bl, full, proj, 0, V, 0, H);
   if (rc) return rc;
-  return launch_remove_incons(s, V, W, H, aw, bl, fuse, full, proj, out, z0, z1);
+  return launch_remove_incons(s, V, W, H, aw, bl, fuse, full, proj, out, z0, z1, 0, H, false);
 }
 
 }  // namespace mvs

@@ -26,9 +26,12 @@ exchange exactly what later stages read from other views:
                                                               49 KB/view)
   propagate (a13) x no_prop         neighbours' state         all-gather state every
                                                               iteration
-  fusion (a14), own block           -                         -
-  projection (a15 i), own block     all disparity maps        all-gather disparity, then
-                                                              all-gather proj
+  fusion (a14), ALL views           every view's spixl,       none: each rank renders
+                                    labels and state          every view from the
+                                                              gathered spixl/labels/state
+                                                              (no refinement: all-gather
+                                                              the disparity maps)
+  projection (a15 i), own block     all disparity maps        all-gather proj
   removal (a15 ii), own block       all proj slices, all      -
                                     disparity maps
 
@@ -162,9 +165,12 @@ class ShardedPipeline:
     EngineBackend for the interface)."""
 
     def __init__(self, backend, settings: params.Settings, cam, gather: ViewGather,
-                 pixel_cost: str | None = "ncc", refine: bool = True, filt: bool = True):
+                 pixel_cost: str | None = "ncc", refine: bool = True, filt: bool = True, proj_bands: int | None = None):
         self.b, self.st, self.cam, self.g = backend, settings, cam, gather
         self.pixel_cost, self.refine, self.filt = pixel_cost, refine, filt
+        # row bands of the pipelined proj all-gather (1: one gather; default: 4
+        # when there is a gather to hide, i.e. world > 1)
+        self.proj_bands = proj_bands if proj_bands is not None else (4 if gather.world > 1 else 1)
 
     def run(self, rgbx: torch.Tensor) -> ShardOutput:
         st, b, g = self.st, self.b, self.g
@@ -189,17 +195,42 @@ class ShardedPipeline:
         out.spixl = g(spixl[z0:z1], spixl)  # centres + seeds (s7) of every view
         out.labels = pending.wait()
         spixl, labels = out.spixl, out.labels
+        full = None
         if self.refine:
-            out.disp_refined = self._refine(spixl, labels, rep, z0, z1)
+            full = self._refine(spixl, labels, rep, z0, z1)
+            out.disp_refined = full[z0:z1]
         if self.filt:
-            src = out.disp_refined if out.disp_refined is not None else out.disp
-            full = g(src)
-            # project_to_reference_inv for the block, then every rank holds all
-            # proj slices, which remove_view_inconsistency reads (clcode.cl:2054)
-            proj = b.proj_inv(full, st.array_width, st.bl_ratio, z0, z1)
-            g(proj[z0:z1], proj)
-            out.disp_filtered = b.remove_inconsistency(full, proj, st.array_width, st.bl_ratio, st.fuse, z0, z1)[z0:z1]
+            if full is None:
+                full = g(out.disp)
+            out.disp_filtered = self._filter(full, z0, z1)
         return out
+
+    def _filter(self, full, z0, z1):
+        """project_to_reference_inv for the block, then every rank holds all proj
+        slices, which remove_view_inconsistency reads (clcode.cl:2054).  The
+        removal at a pixel reads the proj slices at that pixel only, so with
+        proj_bands > 1 the proj all-gather goes in row bands: band c's gather
+        is issued as soon as its rows are projected and runs beside the next
+        bands' projection and the earlier bands' removal."""
+        st, b, g = self.st, self.b, self.g
+        aw, bl, fuse = st.array_width, st.bl_ratio, st.fuse
+        V, H, W = full.shape
+        nb = max(1, min(self.proj_bands, H))
+        if nb == 1:
+            proj = b.proj_inv(full, aw, bl, z0, z1)
+            g(proj[z0:z1], proj)
+            return b.remove_inconsistency(full, proj, aw, bl, fuse, z0, z1)[z0:z1]
+        edges = [(H * i // nb, H * (i + 1) // nb) for i in range(nb)]
+        proj, bands = None, []
+        for ya, yb in edges:
+            proj = b.proj_inv(full, aw, bl, z0, z1, proj=proj, rows=(ya, yb))
+            buf = full.new_empty((V, yb - ya, W))
+            buf[z0:z1] = proj[z0:z1, ya:yb]
+            bands.append((ya, yb, buf, g.start(buf[z0:z1], buf)))
+        res = None
+        for ya, yb, buf, pending in bands:  # the removal reads each gathered band in place
+            res = b.remove_inconsistency(full, pending.wait(), aw, bl, fuse, z0, z1, out=res, rows=(ya, yb), band=True)
+        return res[z0:z1]
 
     def _refine(self, spixl, labels, rep, z0, z1):
         """clDepthRefinement::do_refinement (depth_refinement.cpp:91-118, 724-889)
@@ -219,8 +250,12 @@ class ShardedPipeline:
             b.propagate(spixl, labels, rep, flat, self.cam, st.spixl_size, it, rp["prop_alpha"], rp["prop_gamma"],
                         rp["fuse"], nks, kss, src, dst, z0, z1)
             g(dst[z0:z1], dst)
-        # fusion renders current_state_dev = `state` (Appendix A #13)
-        return b.spixl_to_image(spixl[z0:z1], labels[z0:z1], state[z0:z1], st.spixl_size)
+        # fusion renders current_state_dev = `state` (Appendix A #13).  Every
+        # rank holds every view's spixl, labels and `state` (gathered after
+        # iteration 3), and a fused map is a function of those alone, so each
+        # rank renders ALL views itself (~0.1 ms at C4) instead of all-gathering
+        # the block's maps (8.3 MB per view: 232 MB into every rank at C4).
+        return b.spixl_to_image(spixl, labels, state, st.spixl_size)
 
 
 class EngineBackend:
@@ -273,11 +308,11 @@ class EngineBackend:
     def spixl_to_image(self, spixl, labels, state, S):
         return self.e.spixl_to_image(spixl.contiguous(), labels.contiguous(), state.contiguous(), S)
 
-    def proj_inv(self, disp_full, aw, bl, z0, z1):
-        return self.e.proj_inv(disp_full, aw, bl, z0, z1)
+    def proj_inv(self, disp_full, aw, bl, z0, z1, proj=None, rows=None):
+        return self.e.proj_inv(disp_full, aw, bl, z0, z1, proj=proj, rows=rows)
 
-    def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1):
-        return self.e.remove_inconsistency(disp_full, proj, aw, bl, fuse, z0, z1)
+    def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1, out=None, rows=None, band=False):
+        return self.e.remove_inconsistency(disp_full, proj, aw, bl, fuse, z0, z1, out=out, rows=rows, band=band)
 
 
 def init_from_env(backend: str = "nccl"):

@@ -332,24 +332,41 @@ class Engine:
                                        _ptr(disp_full), _ptr(proj), _ptr(out), int(z0), int(z1)), "mvs_filter_d")
         return proj, out
 
-    def proj_inv(self, disp_full, array_width: int, bl_ratio: float, z0: int, z1: int, proj=None):
-        """project_to_reference_inv for references [z0, z1) into proj[z0:z1] ([V, H, W])."""
+    def proj_inv(self, disp_full, array_width: int, bl_ratio: float, z0: int, z1: int, proj=None, rows=None):
+        """project_to_reference_inv for references [z0, z1) into proj[z0:z1] ([V, H, W]);
+        rows=(y0, y1): image rows [y0, y1) only."""
         V, H, W = disp_full.shape
         proj = self.empty((V, H, W), torch.float32) if proj is None else proj
         self._stream()
-        _lib.check(self.L.mvs_proj_inv_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio), _ptr(disp_full),
-                                         _ptr(proj), int(z0), int(z1)), "mvs_proj_inv_d")
+        if rows is None:
+            _lib.check(self.L.mvs_proj_inv_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio),
+                                             _ptr(disp_full), _ptr(proj), int(z0), int(z1)), "mvs_proj_inv_d")
+        else:
+            _lib.check(self.L.mvs_proj_inv_rows_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio),
+                                                  _ptr(disp_full), _ptr(proj), int(z0), int(z1), int(rows[0]),
+                                                  int(rows[1])), "mvs_proj_inv_rows_d")
         return proj
 
     def remove_inconsistency(self, disp_full, proj, array_width: int, bl_ratio: float, fuse: float, z0: int, z1: int,
-                             out=None):
-        """remove_view_inconsistency for references [z0, z1) (every proj slice filled)."""
+                             out=None, rows=None, band=False):
+        """remove_view_inconsistency for references [z0, z1) (every proj slice filled; rows=(y0, y1):
+        image rows [y0, y1) only, which read only those rows of proj -- with band=True `proj` is
+        that row band alone, [V, y1 - y0, W])."""
         V, H, W = disp_full.shape
         out = torch.zeros((V, H, W), dtype=torch.float32, device=self.device) if out is None else out
+        if band and (rows is None or tuple(proj.shape) != (V, rows[1] - rows[0], W)):
+            raise ValueError("band=True needs rows=(y0, y1) and proj of shape [V, y1 - y0, W]")
         self._stream()
-        _lib.check(self.L.mvs_remove_inconsistency_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio),
-                                                     C.c_float(fuse), _ptr(disp_full), _ptr(proj), _ptr(out),
-                                                     int(z0), int(z1)), "mvs_remove_inconsistency_d")
+        if rows is None:
+            _lib.check(self.L.mvs_remove_inconsistency_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio),
+                                                         C.c_float(fuse), _ptr(disp_full), _ptr(proj), _ptr(out),
+                                                         int(z0), int(z1)), "mvs_remove_inconsistency_d")
+        else:
+            _lib.check(self.L.mvs_remove_inconsistency_rows_d(self.ctx, V, W, H, int(array_width),
+                                                              C.c_float(bl_ratio), C.c_float(fuse), _ptr(disp_full),
+                                                              _ptr(proj), int(bool(band)), _ptr(out), int(z0), int(z1),
+                                                              int(rows[0]), int(rows[1])),
+                       "mvs_remove_inconsistency_rows_d")
         return out
 
     def synchronize(self):

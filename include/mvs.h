@@ -195,6 +195,18 @@ int mvs_proj_inv_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_
                    float* proj, int z0, int z1);
 int mvs_remove_inconsistency_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, float fuse,
                                const float* disp_full, const float* proj, float* out, int z0, int z1);
+/* The same two passes over image rows [y0, y1) only (0 <= y0 <= y1 <= H), for
+ * a shard that pipelines the proj all-gather in row bands: the removal at a
+ * pixel reads the proj slices at that pixel only (clcode.cl:2054-2056), so a
+ * band's removal can start once that band's proj rows have arrived.  The
+ * disparity stack is read in full by both (reprojected gathers).  proj_band
+ * 0: proj is the full [V][H][W] stack; 1: proj is the band alone,
+ * [V][y1 - y0][W] (what a row band's all-gather delivers). */
+int mvs_proj_inv_rows_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, const float* disp_full,
+                        float* proj, int z0, int z1, int y0, int y1);
+int mvs_remove_inconsistency_rows_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, float fuse,
+                                    const float* disp_full, const float* proj, int proj_band, float* out, int z0,
+                                    int z1, int y0, int y1);
 
 /* ---- host-pointer stage API (mirrors the reference stage methods) ------- */
 /* clSLIC::do_super_pixel_seg(in_img, lab_out, spixl_out, idx_out), one view. */

@@ -36,14 +36,19 @@ def main():
         for v in variants:
             k, val = v.split("=")
             os.environ[k] = val
-            for tag, (z0, z1) in (("all32", (0, 32)), ("shard4", (12, 16))):
+            for tag, (z0, z1) in (("all32", (0, 32)), ("shard4", (12, 16)), ("proj32", (0, 32))):
                 s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                _, out = e.filter(full, aw, 1.0, 1.0, z0, z1)
+                if tag == "proj32":
+                    pj = e.proj_inv(full, aw, 1.0, z0, z1)
+                    out = pj
+                else:
+                    pj, out = e.filter(full, aw, 1.0, 1.0, z0, z1)
                 t.record()
                 torch.cuda.synchronize()
                 res.setdefault(f"{v}:{tag}", []).append(s.elapsed_time(t))
-                o = out[z0:z1].cpu().numpy().view(np.uint32)
+                o = np.concatenate([out[z0:z1].cpu().numpy().view(np.uint32).ravel(),
+                                    pj[z0:z1].cpu().numpy().view(np.uint32).ravel()])
                 if tag not in ref:
                     ref[tag] = o
                 elif not np.array_equal(o, ref[tag]):

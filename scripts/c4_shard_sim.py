@@ -85,6 +85,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--save-rec", help="world-1 run only: save the recorded gathers here (torch.save) and exit")
+    ap.add_argument("--load-rec", help="skip the world-1 run: replay the gathers saved by --save-rec")
+    ap.add_argument("--bands", type=int, default=4, help="row bands of the proj all-gather (as at world > 1)")
+    ap.add_argument("--only-rank", type=int, help="run this rank only (e.g. under rocprofv3 --kernel-trace)")
     args = ap.parse_args()
     aw, ah, W, H = 8, 4, 1920, 1080
     V = aw * ah
@@ -96,19 +100,28 @@ def main():
     mat, num = params.flatten_subsets(params.nearest_neighbours(aw, ah, 5))
     cam = CameraArray(aw, 1.0, params.disparity_levels(0, 127, 1), mat, num)
     be = EngineBackend(e, fused=True)
-    rg = RecordingGather(V)
-    sp1 = ShardedPipeline(be, st, cam, rg, pixel_cost="ncc", refine=True, filt=True)
-    ref = sp1.run(rgbx)
-    rec = list(rg.rec)
+    if args.load_rec:
+        saved = torch.load(args.load_rec, weights_only=True)
+        rec = [t.cuda() for t in saved["rec"]]
+        ref_filt, t1 = saved["filt"].cuda(), saved["t1"]
+    else:
+        rg = RecordingGather(V)
+        sp1 = ShardedPipeline(be, st, cam, rg, pixel_cost="ncc", refine=True, filt=True, proj_bands=args.bands)
+        ref_filt = sp1.run(rgbx).disp_filtered
+        rec = list(rg.rec)
+        t1 = timed(lambda: sp1.run(rgbx), args.steps, 1)
+        if args.save_rec:
+            torch.save({"rec": [t.cpu() for t in rec], "filt": ref_filt.cpu(), "t1": t1}, args.save_rec)
+            print(json.dumps({"saved": args.save_rec, "world1_ms_per_step": round(t1, 3)}), flush=True)
+            return
     n_gathers = len(rec)
-    t1 = timed(lambda: sp1.run(rgbx), args.steps, 1)
     ranks = []
-    for r in range(args.world):
+    for r in range(args.world) if args.only_rank is None else [args.only_rank]:
         g = ReplayGather(V, r, args.world, rec)
-        sp = ShardedPipeline(be, st, cam, g, pixel_cost="ncc", refine=True, filt=True)
+        sp = ShardedPipeline(be, st, cam, g, pixel_cost="ncc", refine=True, filt=True, proj_bands=args.bands)
         out = sp.run(rgbx)
         z0, z1 = g.block
-        same = bool(torch.equal(out.disp_filtered.view(torch.int32), ref.disp_filtered[z0:z1].view(torch.int32)))
+        same = bool(torch.equal(out.disp_filtered.view(torch.int32), ref_filt[z0:z1].view(torch.int32)))
         g.bytes_in = 0
         t = timed(lambda: sp.run(rgbx), args.steps, 0)
         ranks.append({"rank": r, "views": [z0, z1], "ms_per_step": round(t, 3), "filtered_bit_identical": same,

@@ -79,18 +79,21 @@ class OracleBackend:
     def spixl_to_image(self, spixl, labels, state, S):
         return torch.from_numpy(orc.spixl_to_image(_np(spixl), _np(labels).view(np.uint32), _np(state), S))
 
-    def proj_inv(self, disp_full, aw, bl, z0, z1):
-        proj, _ = orc.filt(_np(disp_full), aw, bl, 1.0)
-        out = np.full(proj.shape, np.nan, np.float32)
-        out[z0:z1] = proj[z0:z1]
-        return torch.from_numpy(out)
+    def proj_inv(self, disp_full, aw, bl, z0, z1, proj=None, rows=None):
+        oproj, _ = orc.filt(_np(disp_full), aw, bl, 1.0)
+        out = torch.full(oproj.shape, float("nan")) if proj is None else proj
+        ya, yb = rows if rows is not None else (0, oproj.shape[1])
+        out[z0:z1, ya:yb] = torch.from_numpy(oproj[z0:z1, ya:yb])
+        return out
 
-    def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1):
+    def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1, out=None, rows=None, band=False):
         # the oracle filter recomputes every projection itself: check that the
-        # gathered proj the product orchestration hands over equals it
-        oproj, out = orc.filt(_np(disp_full), aw, bl, fuse)
-        if not np.array_equal(_np(proj).view(np.uint32), oproj.view(np.uint32)):
+        # gathered proj rows the product orchestration hands over equal it
+        oproj, filt = orc.filt(_np(disp_full), aw, bl, fuse)
+        ya, yb = rows if rows is not None else (0, oproj.shape[1])
+        got = _np(proj) if band else _np(proj)[:, ya:yb]
+        if not np.array_equal(got.view(np.uint32), oproj[:, ya:yb].view(np.uint32)):
             raise AssertionError("gathered proj slices differ from the full projection")
-        res = torch.zeros_like(disp_full)
-        res[z0:z1] = torch.from_numpy(out[z0:z1])
+        res = torch.zeros_like(disp_full) if out is None else out
+        res[z0:z1, ya:yb] = torch.from_numpy(filt[z0:z1, ya:yb])
         return res

@@ -54,7 +54,7 @@ def _unsharded(c, b):
     return dict(spixl=sp, labels=lb, refined=ref["disp"], filt=filt, disp=disp)
 
 
-def _worker(rank, world, port, name, outdir):
+def _worker(rank, world, port, name, outdir, bands=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -68,7 +68,7 @@ def _worker(rank, world, port, name, outdir):
         st = _settings(c)
         cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
         g = ViewGather(b["V"])
-        pipe = ShardedPipeline(OracleBackend(), st, cam, g, pixel_cost="ncc", refine=True, filt=True)
+        pipe = ShardedPipeline(OracleBackend(), st, cam, g, pixel_cost="ncc", refine=True, filt=True, proj_bands=bands)
         out = pipe.run(torch.from_numpy(b["stack"]))
         np.savez(os.path.join(outdir, f"r{rank}.npz"), z=np.array([out.z0, out.z1]), spixl=out.spixl.numpy(),
                  labels=out.labels.numpy().view(np.uint32), disp=out.disp.numpy(),
@@ -77,12 +77,14 @@ def _worker(rank, world, port, name, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world", [("c3x1_s8", 2), ("c3x1_s8", 3), ("c2x2_s12", 2), ("c3x1_s8", 1)])
-def test_sharded_equals_unsharded(name, world):
+# bands: row bands of the pipelined proj all-gather (None: the default, 4 at world > 1)
+@pytest.mark.parametrize("name,world,bands", [("c3x1_s8", 2, None), ("c3x1_s8", 3, None), ("c2x2_s12", 2, 1),
+                                              ("c3x1_s8", 1, None), ("c3x1_s8", 1, 3)])
+def test_sharded_equals_unsharded(name, world, bands):
     c, b = _case(name)
     want = _unsharded(c, b)
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), name, d), nprocs=world, join=True,
+        mp.start_processes(_worker, args=(world, _free_port(), name, d, bands), nprocs=world, join=True,
                            start_method="spawn")
         seen = []
         for r in range(world):

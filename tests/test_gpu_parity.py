@@ -322,6 +322,41 @@ def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns):
     assert_bits(out.cpu().numpy(), oout, f"filter output ({kern}, FB {fb})")
 
 
+@pytest.mark.parametrize("kern", ["q", "b", "lds", "px"])
+@pytest.mark.parametrize("aw,ah", [(3, 2), (4, 3), (8, 4), (9, 5), (10, 7)])
+def test_filter_row_bands(engine, monkeypatch, aw, ah, kern):
+    # mvs_proj_inv_rows_d / mvs_remove_inconsistency_rows_d (the sharded
+    # pipeline's banded proj all-gather): uneven row bands, every band written
+    # into shared proj / out buffers, tile the full-range result for every
+    # removal kernel (V = 6, 12, 32, 45, 70; the 16 < V <= 32 kernels forced
+    # per call) and every projection variant (MVS_PROJ_NC rows per thread,
+    # bands not a multiple of it)
+    V, H, W = aw * ah, 23, 70
+    if kern != "q" and V != 32:
+        pytest.skip("removal kernel variants apply at 16 < V <= 32")
+    rng = np.random.default_rng(aw * 13 + ah)
+    base = rng.integers(2, 9, size=(V, 1, 1)).astype(np.float32)
+    disp = base + rng.choice(np.float32([0.0, 0.5, 1.0, 3.0]), size=(V, H, W))
+    disp[rng.random(disp.shape) < 0.1] = 0.0
+    d = dev(disp)
+    monkeypatch.setenv("MVS_FILTER_KERNEL", kern)
+    oproj, oout = orc.filt(disp, aw, 1.0359, 1.0)
+    bands = [(0, 5), (5, 6), (6, 17), (17, 17), (17, 23)]
+    for nc in ("1", "2", "4", "8"):
+        monkeypatch.setenv("MVS_PROJ_NC", nc)
+        proj = torch.full((V, H, W), float("nan"), device=d.device)
+        for ya, yb in bands:
+            engine.proj_inv(d, aw, 1.0359, 0, V, proj=proj, rows=(ya, yb))
+        assert_bits(proj.cpu().numpy(), oproj, f"banded projection (NC {nc})")
+    for band in (False, True):  # proj rows within the full stack / the band alone, [V, yb - ya, W]
+        out = torch.full((V, H, W), -1.0, device=d.device)
+        for z0, z1 in ((0, V // 3), (V // 3, V)):
+            for ya, yb in bands:
+                pj = proj[:, ya:yb].contiguous() if band else proj
+                engine.remove_inconsistency(d, pj, aw, 1.0359, 1.0, z0, z1, out=out, rows=(ya, yb), band=band)
+        assert_bits(out.cpu().numpy(), oout, f"banded removal ({kern}, band buffer {band})")
+
+
 def test_determinism(engine):
     c = CASES["c5x1_s32"]
     b = build(c)

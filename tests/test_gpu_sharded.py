@@ -22,14 +22,15 @@ def bits(a):
     return a.view(np.uint32) if a.dtype in (np.float32, np.int32) else a
 
 
-@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("fused,bands", [(False, None), (True, None), (True, 3)])
 @pytest.mark.parametrize("name", ["c3x1_s8", "c2x2_s12"])
-def test_sharded_pipeline_world1(engine, name, fused):
+def test_sharded_pipeline_world1(engine, name, fused, bands):
     c = dict(CASES[name])
     b = build(c)
     want = _unsharded(c, b)
     cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
-    pipe = ShardedPipeline(EngineBackend(engine, fused=fused), _settings(c), cam, ViewGather(b["V"]))
+    pipe = ShardedPipeline(EngineBackend(engine, fused=fused), _settings(c), cam, ViewGather(b["V"]),
+                           proj_bands=bands)
     out = pipe.run(torch.from_numpy(b["stack"]).cuda())
     assert np.array_equal(bits(out.labels), want["labels"])
     assert np.array_equal(bits(out.spixl), want["spixl"].view(np.uint32))

@@ -694,6 +694,44 @@ __global__ void k_spixl_to_image(const float* __restrict__ spixl, const uint32_t
   disp[P * z + (long)W * y + x] = v / t[5];
 }
 
+// The same map, 4 consecutive pixels per thread (W % 4 == 0): one 16-B label
+// load and one 16-B store per thread, the record gathers as buffer loads
+// with 32-bit offsets inside view z's records (a label is the superpixel
+// index sy * mw + sx, so the record is at M * z + label, as in
+// comp_consistency).  Same arithmetic per pixel.
+__global__ __launch_bounds__(256) void k_spixl_to_image4(const float* __restrict__ spixl,
+                                                         const uint32_t* __restrict__ labels,
+                                                         const float* __restrict__ st, int W, int H, int mw, int mh,
+                                                         float* __restrict__ disp) {
+  const int x = 4 * (blockIdx.x * blockDim.x + threadIdx.x), y = blockIdx.y, z = blockIdx.z;
+  if (x >= W) return;
+  const long M = (long)mw * mh, P = (long)W * H, p = P * z + (long)W * y + x;
+  const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc((void*)(spixl + 8 * M * z), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc((void*)(st + 6 * M * z), 0, 0x7fffffff, 0x00020000);
+  const uint4 id4 = *(const uint4*)(labels + p);
+  const unsigned ids[4] = {id4.x, id4.y, id4.z, id4.w};
+  float s1[4], s2[4], t0[4], t3[4], t4[4], t5[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int os = (int)ids[k] * 32, ot = (int)ids[k] * 24;
+    s1[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsp, os + 4, 0, 0));
+    s2[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsp, os + 8, 0, 0));
+    t0[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot, 0, 0));
+    t3[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot + 12, 0, 0));
+    t4[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot + 16, 0, 0));
+    t5[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot + 20, 0, 0));
+  }
+  float o[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    float v = t3[k] * (s1[k] - (float)(x + k));
+    v = v + t4[k] * (s2[k] - (float)y);
+    v = v + t5[k] * t0[k];
+    o[k] = v / t5[k];
+  }
+  *(float4*)(disp + p) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
 // ---- cross-view filter -------------------------------------------------------
 __device__ __forceinline__ float round_ha(float v);
 // Filter grid orders.  RM = false: (x tiles, rows, reference groups), so a
@@ -1498,8 +1536,13 @@ int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl
 int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
                           const float* state, float* disp) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
-  hipLaunchKernelGGL(k_spixl_to_image, dim3((W + 255) / 256, H, V), dim3(256), 0, s, spixl, labels, state, W, H,
-                     mw, mh, disp);
+  // the 4-pixel form needs 16-B aligned rows and 32-bit record offsets
+  if (W % 4 == 0 && (long)mw * mh * 32 < (1L << 31) && ((uintptr_t)labels & 15) == 0 && ((uintptr_t)disp & 15) == 0)
+    hipLaunchKernelGGL(k_spixl_to_image4, dim3((W / 4 + 255) / 256, H, V), dim3(256), 0, s, spixl, labels, state, W,
+                       H, mw, mh, disp);
+  else
+    hipLaunchKernelGGL(k_spixl_to_image, dim3((W + 255) / 256, H, V), dim3(256), 0, s, spixl, labels, state, W, H,
+                       mw, mh, disp);
   MVS_LAUNCH_CHECK("k_spixl_to_image");
   return 0;
 }

@@ -141,8 +141,9 @@ class PendingGather:
 
 
 def _expand(blk: torch.Tensor, V: int, z0: int) -> torch.Tensor:
-    """[V, ...] zeros holding `blk` at views [z0, z0 + len(blk))."""
-    full = blk.new_zeros((V,) + tuple(blk.shape[1:]))
+    """[V, ...] holding `blk` at views [z0, z0 + len(blk)); the other views are
+    left unset (an all-gather fills them before any stage reads them)."""
+    full = blk.new_empty((V,) + tuple(blk.shape[1:]))
     full[z0:z0 + blk.shape[0]] = blk
     return full
 
@@ -168,9 +169,9 @@ class ShardedPipeline:
                  pixel_cost: str | None = "ncc", refine: bool = True, filt: bool = True, proj_bands: int | None = None):
         self.b, self.st, self.cam, self.g = backend, settings, cam, gather
         self.pixel_cost, self.refine, self.filt = pixel_cost, refine, filt
-        # row bands of the pipelined proj all-gather (1: one gather; default: 4
+        # row bands of the pipelined proj all-gather (1: one gather; default: 2
         # when there is a gather to hide, i.e. world > 1)
-        self.proj_bands = proj_bands if proj_bands is not None else (4 if gather.world > 1 else 1)
+        self.proj_bands = proj_bands if proj_bands is not None else (2 if gather.world > 1 else 1)
 
     def run(self, rgbx: torch.Tensor) -> ShardOutput:
         st, b, g = self.st, self.b, self.g
@@ -216,10 +217,11 @@ class ShardedPipeline:
         aw, bl, fuse = st.array_width, st.bl_ratio, st.fuse
         V, H, W = full.shape
         nb = max(1, min(self.proj_bands, H))
+        res = full.new_empty(full.shape)  # only the block's views are written
         if nb == 1:
             proj = b.proj_inv(full, aw, bl, z0, z1)
             g(proj[z0:z1], proj)
-            return b.remove_inconsistency(full, proj, aw, bl, fuse, z0, z1)[z0:z1]
+            return b.remove_inconsistency(full, proj, aw, bl, fuse, z0, z1, out=res)[z0:z1]
         edges = [(H * i // nb, H * (i + 1) // nb) for i in range(nb)]
         proj, bands = None, []
         for ya, yb in edges:
@@ -227,7 +229,6 @@ class ShardedPipeline:
             buf = full.new_empty((V, yb - ya, W))
             buf[z0:z1] = proj[z0:z1, ya:yb]
             bands.append((ya, yb, buf, g.start(buf[z0:z1], buf)))
-        res = None
         for ya, yb, buf, pending in bands:  # the removal reads each gathered band in place
             res = b.remove_inconsistency(full, pending.wait(), aw, bl, fuse, z0, z1, out=res, rows=(ya, yb), band=True)
         return res[z0:z1]

@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--save-rec", help="world-1 run only: save the recorded gathers here (torch.save) and exit")
     ap.add_argument("--load-rec", help="skip the world-1 run: replay the gathers saved by --save-rec")
-    ap.add_argument("--bands", type=int, default=4, help="row bands of the proj all-gather (as at world > 1)")
+    ap.add_argument("--bands", type=int, default=2, help="row bands of the proj all-gather (as at world > 1)")
     ap.add_argument("--only-rank", type=int, help="run this rank only (e.g. under rocprofv3 --kernel-trace)")
     args = ap.parse_args()
     aw, ah, W, H = 8, 4, 1920, 1080

@@ -77,7 +77,7 @@ def _worker(rank, world, port, name, outdir, bands=None):
         dist.destroy_process_group()
 
 
-# bands: row bands of the pipelined proj all-gather (None: the default, 4 at world > 1)
+# bands: row bands of the pipelined proj all-gather (None: the default, 2 at world > 1)
 @pytest.mark.parametrize("name,world,bands", [("c3x1_s8", 2, None), ("c3x1_s8", 3, None), ("c2x2_s12", 2, 1),
                                               ("c3x1_s8", 1, None), ("c3x1_s8", 1, 3)])
 def test_sharded_equals_unsharded(name, world, bands):

@@ -48,7 +48,8 @@ CONFIGS = {
     "c4": dict(aw=8, ah=4, W=1920, H=1080, S=32, dmin=0, dmax=127, K=5, nh=0, nv=0, knn=5, bl=1.0, cost="ncc",
                refine=True, filt=True, sharded=True,
                workload="32 reference views x 5 nearest neighbours, 1080p, one array sharded by reference view over "
-                        "the GPUs (RCCL all-gathers of labels/spixl, refinement state, disparity, projections)"),
+                        "the GPUs (RCCL all-gathers of labels/spixl and refinement state, fused maps rendered per "
+                        "rank, projections gathered in row bands)"),
     # the reference's own defaults (clMVDE.cpp main): its algorithm exactly, no per-pixel sweep
     "ref": dict(aw=3, ah=3, W=1920, H=1080, S=8, dmin=30, dmax=60, K=5, nh=1, nv=1, bl=1.0359, cost="none",
                 refine=True,

@@ -764,16 +764,25 @@ __global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full
   const int crx = r % aw, cry = r / aw;
   const float xf = (float)x, yf = (float)y;
   float md = full[P * r + p];
-  for (int i = 0; i < V; i++) {
-    if (i == r) continue;
-    const int cx = i % aw, cy = i / aw;
-    const int xp = (int)(xf - round_ha(md * (float)(crx - cx)));
-    const int yp = (int)(yf - round_ha((bl * md) * (float)(cry - cy)));
-    const bool in = (unsigned)xp < (unsigned)W && (unsigned)yp < (unsigned)H;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(full + P * i), 0, 0x7fffffff, 0x00020000);
-    const int off = in ? (int)((unsigned)yp * (unsigned)W + (unsigned)xp) * 4 : 0x7fffffff;
-    const float cd = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-    if (in && md < cd) md = cd;
+  // camera column / row of view i kept incrementally (scalar): i % aw and i / aw
+  // per view were ~25 SALU instructions each, 0.86 G per C4 launch -- as many
+  // SALU cycles per CU as the loop's VALU cycles per SIMD
+  int cx = 0, cy = 0;
+  const float* vb = full;
+  for (int i = 0; i < V; i++, vb += P) {
+    if (i != r) {
+      const int xp = (int)(xf - round_ha(md * (float)(crx - cx)));
+      const int yp = (int)(yf - round_ha((bl * md) * (float)(cry - cy)));
+      const bool in = (unsigned)xp < (unsigned)W && (unsigned)yp < (unsigned)H;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)vb, 0, 0x7fffffff, 0x00020000);
+      const int off = in ? (int)((unsigned)yp * (unsigned)W + (unsigned)xp) * 4 : 0x7fffffff;
+      const float cd = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+      if (in && md < cd) md = cd;
+    }
+    if (++cx == aw) {
+      cx = 0;
+      cy++;
+    }
   }
   proj[P * r + p] = md;
 }

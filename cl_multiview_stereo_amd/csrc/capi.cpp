@@ -330,6 +330,15 @@ int mvs_ncc_wta_d(mvs_ctx* c, int W, int H, const uint8_t* l8, const int32_t* bo
                                 a->subset_num, a->array_width, a->bl_ratio, K, z, nullptr, c->d_levels, disp, conf);
 }
 
+int mvs_ncc_wta_range_d(mvs_ctx* c, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a, int K,
+                        int z0, int z1, float* disp, float* conf) {
+  if (!c || !l8 || !box || !disp || bad_dims(W, H)) return mvs::arg_fail("mvs_ncc_wta_range_d: bad arguments");
+  RC(upload_meta(c, a));
+  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_ncc_wta_range_d: bad view range");
+  return mvs::launch_ncc_refs(c, a->view_count, W, H, box, a->levels, a->num_levels, a->view_subset, a->subset_num,
+                              a->array_width, a->bl_ratio, K, z0, z1, nullptr, c->d_levels, disp, conf);
+}
+
 int mvs_wta_d(mvs_ctx* c, int W, int H, int D, const float* vol, const float* levels, float* disp, float* conf) {
   if (!c || !vol || !levels || !disp || D <= 0 || bad_dims(W, H)) return mvs::arg_fail("mvs_wta_d: bad arguments");
   return mvs::launch_wta(c->stream, W, H, D, vol, levels, disp, conf);

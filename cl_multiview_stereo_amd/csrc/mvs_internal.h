@@ -89,6 +89,9 @@ int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int 
 int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
                       const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol,
                       const float* levels_dev = nullptr, float* disp = nullptr, float* conf = nullptr);
+int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
+                    const int* vs_host, const int* sn_host, int aw, float bl, int K, int z0, int z1, float* vol,
+                    const float* levels_dev, float* disp, float* conf);
 int launch_wta(hipStream_t s, int W, int H, int D, const float* vol, const float* levels, float* disp,
                float* conf);
 

@@ -39,6 +39,8 @@
 //     plane are one 16-byte LDS read), then v_max_f32 per cell;
 //   * the chunk's costs are written once, 64-column coalesced rows.
 #include <algorithm>
+#include <array>
+#include <vector>
 #include <type_traits>
 #include <cstdlib>
 
@@ -108,12 +110,16 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
 }
 
 constexpr int kMaxNbr = 16;
+constexpr int kMaxRef = 8;  // reference views per launch (the fused sweep takes a run of them)
 constexpr int kCPolNT = 2;  // buffer cache policy: non-temporal (CPol::NT on gfx940+)
 struct NccArgs {
-  int W, H, D, nn, z;
-  int tiles_x, ntiles, tiles_per_xcd, nch;  // XCD-aware work map (see k_ncc_volume)
-  int view[kMaxNbr];
+  int W, H, D, nref;
+  int tiles_x, ntiles, tiles_per_xcd, nch;  // XCD-aware work map over nref x ntiles tiles (see k_ncc_volume)
   int pk_pairs, st_pairs;  // LDS band heights in row pairs; the pair-row stride is the template BW
+  // per reference view r of the launch: view id, neighbour count, first plan
+  // record, neighbour view ids
+  int z[kMaxRef], nn[kMaxRef], plan[kMaxRef];
+  int view[kMaxRef][kMaxNbr];
 };
 // host-built plan (device memory, cached per context): one 128-B record per
 // (chunk c, neighbour n, wave w), read with one scalar load per neighbour.
@@ -259,14 +265,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // XCD-aware map: blocks are dealt round-robin over the 8 XCDs, so block b
   // works in XCD-group b % 8; each group takes a contiguous strip of tiles,
   // whose neighbour bands and halos then overlap in its L2.
+  // Several reference views per launch (fused sweep): the tiles of reference
+  // r of the launch are r * ntiles .. r * ntiles + ntiles - 1, one kernel
+  // boundary for the run instead of one per view.
   const int bid = blockIdx.x, grp = bid & 7;
-  const int tile = grp * a.tiles_per_xcd + (bid >> 3);
-  if (tile >= a.ntiles) return;  // padding block (whole workgroup, before any barrier)
+  const int tg = grp * a.tiles_per_xcd + (bid >> 3);
+  if (tg >= a.ntiles * a.nref) return;  // padding block (whole workgroup, before any barrier)
+  const int ref = tg / a.ntiles, tile = tg - ref * a.ntiles;
   const int x0 = (tile % a.tiles_x) * 64;
   const int y0 = (tile / a.tiles_x) * TH;  // even
   const int x = x0 + lane;
-  const int nn = a.nn, T = a.nch * nn;   // pipeline steps
-  const NccRec* rec = plan + wave;       // record of step t = c*nn + n for this wave at rec[NW * t]
+  const int nn = a.nn[ref], T = a.nch * nn;  // pipeline steps
+  const NccRec* rec = plan + a.plan[ref] + wave;  // record of step t = c*nn + n for this wave at rec[NW * t]
 
   // LDS-DMA staging of step t's neighbour bands into buffer b.  Band column j
   // is image column x0 - txmax + j; band pair row i of pk holds image rows
@@ -277,7 +287,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     const NccRec& e = rec[NW * t];
     const int bhp = e.bhp, shp = e.shp & 0xffff, nblk = e.shp >> 16;
     const int pm0 = (y0 - R - e.tymax) >> 1, sm0 = (y0 - e.tymax) >> 1;
-    const long vo = (long)a.view[n] * Pv;
+    const long vo = (long)a.view[ref][n] * Pv;
     u32x4* npk = nbase + b * nbuf;
     u32x4* nst = npk + a.pk_pairs * BW;
     for (int cb = 0; cb < nblk; cb++) {
@@ -364,7 +374,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   stage(0, 0, 0);
   // reference: packed rows y0-R .. y0+TH+R-1 in registers; its centred window
   // sums Sr' and 1/sqrt(var_r) from them (dot4 with ones / with itself)
-  const long zo = (long)a.z * Pv;
+  const long zo = (long)a.z[ref] * Pv;
   const int xc = min(x, W - 1);
   unsigned qlo[NR], qhi[NR];
   int rsum[NR], rsq[NR];
@@ -482,7 +492,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
         c2 = vmin(c2, v);
       }
       if (xx < W && yy < H) {
-        const long p = (long)yy * W + xx;
+        const long p = P * ref + (long)yy * W + xx;  // disp / conf of reference r of the launch
         wo.disp[p] = bi >= 0 ? wo.levels[bi] : 0.0f;
         if (wo.conf) wo.conf[p] = (bi < 0 || c2 == kWtaInit) ? 0.0f : c2 - bv;
       }
@@ -560,7 +570,7 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
   constexpr int DC = NW * DPW;
   a.tiles_x = (a.W + 63) / 64;
   a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);
-  a.tiles_per_xcd = (a.ntiles + 7) / 8;
+  a.tiles_per_xcd = (a.nref * a.ntiles + 7) / 8;
   a.nch = (a.D + DC - 1) / DC;
   dim3 g(8 * a.tiles_per_xcd);
   auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, EVEN, false> : k_ncc_volume<K, TH, DPW, NW, BW, EVEN, true>;
@@ -573,31 +583,92 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
   return 0;
 }
 
-// returns 1 if this variant does not fit the LDS (caller tries a smaller one)
-template <int K, int TH, int DPW, int NW>
-int launch_ncc_t(mvs_ctx* ctx, const uint2* stats, const uint2* pk, NccArgs& a, const float* levels_host,
-                 const float* fdx, const float* fdy, float bl, float* vol, const WtaOut& wo, size_t lds_cap) {
-  NccPlan p = make_plan<K, TH, DPW, NW>(levels_host, a.D, a.nn, fdx, fdy, bl);
+// One reference view's variant: its shift plan for (K, TH = 8, DPW, NW) and
+// the band pair-row stride, if its double-buffered bands fit `cap` bytes of LDS.
+struct NccChoice {
+  int dpw = 0, nw = 0, bwt = 0;
+  size_t cap = 0;
+  NccPlan plan;
+};
+template <int K, int DPW, int NW>
+bool try_plan(const mvs_ctx* ctx, const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl,
+              size_t cap, NccChoice& o) {
+  NccPlan p = make_plan<K, 8, DPW, NW>(levels, D, nn, fdx, fdy, bl);
   // the band's pair-row stride is the template BW: the smallest of 128 / 192 /
   // 256 holding band_w, or a wider one forced through mvs_set_ncc_variant
   const int bw = std::max(std::max(p.band_w, ctx->ncc_bw), 128);
   const int bwt = bw <= 128 ? 128 : bw <= 192 ? 192 : 256;
   const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * bwt;
-  if (lds > lds_cap || bw > 256) return 1;
-  int rc = 0;
-  const int32_t* dev = plan_upload(ctx, p.table, &rc);
-  if (rc) return rc;
-  a.pk_pairs = p.pk_pairs;
-  a.st_pairs = p.st_pairs;
-  const NccRec* plan = (const NccRec*)dev;
-  if (p.even && !ctx->ncc_general) {
-    if (bwt == 128) return launch_ncc_bw<K, TH, DPW, NW, 128, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-    if (bwt == 192) return launch_ncc_bw<K, TH, DPW, NW, 192, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-    return launch_ncc_bw<K, TH, DPW, NW, 256, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (lds > cap || bw > 256) return false;
+  o.dpw = DPW;
+  o.nw = NW;
+  o.bwt = bwt;
+  o.cap = cap;
+  o.plan = std::move(p);
+  return true;
+}
+// waves per workgroup and levels per wave: MVS_NCC_NW (4|8), MVS_NCC_DPW
+// (1|2|4), or the context's override (mvs_set_ncc_variant), tried first.
+// Then the widest variant whose double-buffered bands leave room for two
+// workgroups per CU (vertical shifts grow the bands: fewer levels per step
+// then beat a single resident workgroup), then any that fits the LDS.
+template <int K>
+bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, const float* fdx, const float* fdy,
+                    float bl, NccChoice& o) {
+  static const int dpw_env = [] {
+    const char* e = getenv("MVS_NCC_DPW");
+    return e ? atoi(e) : 4;
+  }();
+  static const int nw_env = [] {
+    const char* e = getenv("MVS_NCC_NW");
+    return e ? atoi(e) : 8;
+  }();
+  const int dpw_pref = ctx->ncc_dpw ? ctx->ncc_dpw : dpw_env;
+  const int nw_pref = ctx->ncc_nw ? ctx->ncc_nw : nw_env;
+  bool ok = false;
+#define MVS_NCC_TRY(DD, WW) \
+  if (!ok) ok = try_plan<K, DD, WW>(ctx, levels, D, nn, fdx, fdy, bl, cap, o);
+  if (ctx->ncc_nw || ctx->ncc_dpw) {  // a forced variant is tried first, at the full LDS
+    const size_t cap = (size_t)160 * 1024;
+    if (nw_pref >= 8 && dpw_pref >= 4) {
+      MVS_NCC_TRY(4, 8)
+    } else if (dpw_pref >= 4) {
+      MVS_NCC_TRY(4, 4)
+    } else if (dpw_pref >= 2) {
+      MVS_NCC_TRY(2, 4)
+    } else {
+      MVS_NCC_TRY(1, 4)
+    }
   }
-  if (bwt == 128) return launch_ncc_bw<K, TH, DPW, NW, 128, false>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 192) return launch_ncc_bw<K, TH, DPW, NW, 192, false>(ctx, stats, pk, plan, a, vol, wo, lds);
-  return launch_ncc_bw<K, TH, DPW, NW, 256, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+  for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
+    if (nw_pref >= 8 && dpw_pref >= 4) MVS_NCC_TRY(4, 8)
+    if (dpw_pref >= 4) MVS_NCC_TRY(4, 4)
+    if (dpw_pref >= 2) MVS_NCC_TRY(2, 4)
+    MVS_NCC_TRY(1, 4)
+  }
+#undef MVS_NCC_TRY
+  return ok;
+}
+
+template <int K, int DPW, int NW>
+int launch_bw_even(mvs_ctx* ctx, int bwt, bool even, const uint2* stats, const uint2* pk, const NccRec* plan,
+                   NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
+  if (even && !ctx->ncc_general) {
+    if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+    if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+    return launch_ncc_bw<K, 8, DPW, NW, 256, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+  }
+  if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+  return launch_ncc_bw<K, 8, DPW, NW, 256, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+}
+template <int K>
+int launch_variant(mvs_ctx* ctx, const NccChoice& c, int bwt, bool even, const uint2* stats, const uint2* pk,
+                   const NccRec* plan, NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
+  if (c.dpw == 4 && c.nw == 8) return launch_bw_even<K, 4, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 4) return launch_bw_even<K, 4, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 2) return launch_bw_even<K, 2, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
+  return launch_bw_even<K, 1, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
 }
 
 }  // namespace
@@ -617,88 +688,94 @@ int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int 
   return 0;
 }
 
-int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
-                      const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol,
-                      const float* levels_dev, float* disp, float* conf) {
+// Reference views [z0, z1): each view's variant is chosen on its own shifts;
+// runs of consecutive views with the same (DPW, NW) whose merged bands still
+// fit every member's LDS cap share one launch (up to kMaxRef views, fused
+// sweep only: a cost volume holds one view), with the widest band stride and
+// EVEN only when every member's rows start on pairs -- the same arithmetic,
+// one kernel boundary (~11 us between two of these launches) per run.
+int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
+                    const int* vs_host, const int* sn_host, int aw, float bl, int K, int z0, int z1, float* vol,
+                    const float* levels_dev, float* disp, float* conf) {
   if (!vol && (!levels_dev || !disp)) return arg_fail("fused NCC sweep needs levels and disp");
-  const WtaOut wo{levels_dev, disp, conf};
+  if (vol && z1 - z0 != 1) return arg_fail("the NCC cost volume holds one reference view");
   if (W < 2) return arg_fail("NCC sweep needs W >= 2");
-  NccArgs a{};
-  a.W = W; a.H = H; a.D = D; a.z = z;
-  a.nn = sn_host[z];
-  if (a.nn > kMaxNbr) return arg_fail("NCC sweep supports at most 16 neighbours per reference view");
-  float fdx[kMaxNbr], fdy[kMaxNbr];
-  int rx = z % aw, ry = z / aw;
-  for (int n = 0; n < a.nn; n++) {
-    int v = vs_host[V * z + n];
-    if (v < 0 || v >= V) return arg_fail("view_subset entry out of range");
-    a.view[n] = v;
-    fdx[n] = (float)(v % aw - rx);
-    fdy[n] = (float)(v / aw - ry);
+  if (K != 5 && K != 7) return arg_fail("NCC window must be 5 or 7");
+  const int n = z1 - z0;
+  if (n <= 0) return 0;
+  std::vector<NccChoice> ch(n);
+  std::vector<std::array<int, kMaxNbr>> views(n);
+  for (int r = 0; r < n; r++) {
+    const int z = z0 + r, nn = sn_host[z];
+    if (nn > kMaxNbr) return arg_fail("NCC sweep supports at most 16 neighbours per reference view");
+    float fdx[kMaxNbr], fdy[kMaxNbr];
+    const int rx = z % aw, ry = z / aw;
+    for (int k = 0; k < nn; k++) {
+      const int v = vs_host[V * z + k];
+      if (v < 0 || v >= V) return arg_fail("view_subset entry out of range");
+      views[r][k] = v;
+      fdx[k] = (float)(v % aw - rx);
+      fdy[k] = (float)(v / aw - ry);
+    }
+    const bool ok = K == 5 ? choose_variant<5>(ctx, levels_host, D, nn, fdx, fdy, bl, ch[r])
+                           : choose_variant<7>(ctx, levels_host, D, nn, fdx, fdy, bl, ch[r]);
+    if (!ok) return arg_fail("NCC sweep: neighbour shifts too large for the LDS band");
   }
   const uint2* stats = (const uint2*)box;
   const uint2* pk = stats + (long)V * W * (H + (H & 1));
-  // waves per workgroup and levels per wave: MVS_NCC_NW (4|8), MVS_NCC_DPW (1|2|4)
-  static const int dpw_env = [] {
-    const char* e = getenv("MVS_NCC_DPW");
-    return e ? atoi(e) : 4;
-  }();
-  static const int nw_env = [] {
-    const char* e = getenv("MVS_NCC_NW");
-    return e ? atoi(e) : 8;
-  }();
-  // per-context override (mvs_set_ncc_variant): the first variant tried
-  const int dpw_pref = ctx->ncc_dpw ? ctx->ncc_dpw : dpw_env;
-  const int nw_pref = ctx->ncc_nw ? ctx->ncc_nw : nw_env;
-  int rc = 1;
-  // first the widest variant whose double-buffered bands leave room for two
-  // workgroups per CU (vertical shifts grow the bands: fewer levels per step
-  // then beat a single resident workgroup), then any that fits the LDS
-#define MVS_NCC_TRY(KK, DD, WW)                                                                     \
-  if (rc == 1) rc = launch_ncc_t<KK, 8, DD, WW>(ctx, stats, pk, a, levels_host, fdx, fdy, bl, vol, wo, cap);
-  // a variant forced through mvs_set_ncc_variant is tried first, at the full LDS
-  if (ctx->ncc_nw || ctx->ncc_dpw) {
-    const size_t cap = (size_t)160 * 1024;
-    if (K == 5) {
-      if (nw_pref >= 8 && dpw_pref >= 4) {
-        MVS_NCC_TRY(5, 4, 8)
-      } else if (dpw_pref >= 4) {
-        MVS_NCC_TRY(5, 4, 4)
-      } else if (dpw_pref >= 2) {
-        MVS_NCC_TRY(5, 2, 4)
-      } else {
-        MVS_NCC_TRY(5, 1, 4)
-      }
-    } else if (K == 7) {
-      if (nw_pref >= 8 && dpw_pref >= 4) {
-        MVS_NCC_TRY(7, 4, 8)
-      } else if (dpw_pref >= 4) {
-        MVS_NCC_TRY(7, 4, 4)
-      } else if (dpw_pref >= 2) {
-        MVS_NCC_TRY(7, 2, 4)
-      } else {
-        MVS_NCC_TRY(7, 1, 4)
-      }
+  constexpr int RW = sizeof(NccRec) / 4;
+  const long P = (long)W * H;
+  for (int i = 0; i < n;) {
+    int bwt = ch[i].bwt, pkp = ch[i].plan.pk_pairs, stp = ch[i].plan.st_pairs;
+    bool even = ch[i].plan.even;
+    size_t cap = ch[i].cap;
+    int j = i + 1;
+    while (!vol && j < n && j - i < kMaxRef && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw) {
+      const int b2 = std::max(bwt, ch[j].bwt);
+      const int p2 = std::max(pkp, ch[j].plan.pk_pairs), s2 = std::max(stp, ch[j].plan.st_pairs);
+      const size_t c2 = std::min(cap, ch[j].cap);
+      if (2 * 16 * (size_t)(p2 + s2) * b2 > c2) break;
+      bwt = b2;
+      pkp = p2;
+      stp = s2;
+      cap = c2;
+      even = even && ch[j].plan.even;
+      j++;
     }
-  }
-  for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
-    if (K == 5) {
-      if (nw_pref >= 8 && dpw_pref >= 4) MVS_NCC_TRY(5, 4, 8)
-      if (dpw_pref >= 4) MVS_NCC_TRY(5, 4, 4)
-      if (dpw_pref >= 2) MVS_NCC_TRY(5, 2, 4)
-      MVS_NCC_TRY(5, 1, 4)
-    } else if (K == 7) {
-      if (nw_pref >= 8 && dpw_pref >= 4) MVS_NCC_TRY(7, 4, 8)
-      if (dpw_pref >= 4) MVS_NCC_TRY(7, 4, 4)
-      if (dpw_pref >= 2) MVS_NCC_TRY(7, 2, 4)
-      MVS_NCC_TRY(7, 1, 4)
-    } else {
-      return arg_fail("NCC window must be 5 or 7");
+    NccArgs a{};
+    a.W = W;
+    a.H = H;
+    a.D = D;
+    a.nref = j - i;
+    a.pk_pairs = pkp;
+    a.st_pairs = stp;
+    std::vector<int32_t> table;
+    for (int r = i; r < j; r++) {
+      const int z = z0 + r;
+      a.z[r - i] = z;
+      a.nn[r - i] = sn_host[z];
+      a.plan[r - i] = (int)(table.size() / RW);
+      for (int k = 0; k < sn_host[z]; k++) a.view[r - i][k] = views[r][k];
+      table.insert(table.end(), ch[r].plan.table.begin(), ch[r].plan.table.end());
     }
+    int rc = 0;
+    const int32_t* dev = plan_upload(ctx, table, &rc);
+    if (rc) return rc;
+    const WtaOut wo{levels_dev, disp ? disp + P * i : nullptr, conf ? conf + P * i : nullptr};
+    const size_t lds = 2 * 16 * (size_t)(pkp + stp) * bwt;
+    rc = K == 5 ? launch_variant<5>(ctx, ch[i], bwt, even, stats, pk, (const NccRec*)dev, a, vol, wo, lds)
+                : launch_variant<7>(ctx, ch[i], bwt, even, stats, pk, (const NccRec*)dev, a, vol, wo, lds);
+    if (rc) return rc;
+    i = j;
   }
-#undef MVS_NCC_TRY
-  if (rc == 1) return arg_fail("NCC sweep: neighbour shifts too large for the LDS band");
-  return rc;
+  return 0;
+}
+
+int launch_ncc_volume(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
+                      const int* vs_host, const int* sn_host, int aw, float bl, int K, int z, float* vol,
+                      const float* levels_dev, float* disp, float* conf) {
+  return launch_ncc_refs(ctx, V, W, H, box, levels_host, D, vs_host, sn_host, aw, bl, K, z, z + 1, vol, levels_dev,
+                         disp, conf);
 }
 
 }  // namespace mvs

@@ -234,6 +234,24 @@ class Engine:
                                         _ptr(conf) if want_conf else None), "mvs_ncc_wta_d")
         return disp, conf
 
+    def ncc_wta_range(self, l8, box, cam: CameraArray, z0: int, z1: int, K: int = 5, disp=None, conf=None,
+                      want_conf: bool = True):
+        """ncc_wta for reference views [z0, z1) into disp/conf [z1 - z0, H, W]; views sharing a
+        sweep variant go in one launch (bit-identical to one ncc_wta per view)."""
+        V, H, W = l8.shape
+        n = z1 - z0
+        disp = self.empty((n, H, W), torch.float32) if disp is None else disp
+        if want_conf and conf is None:
+            conf = self.empty((n, H, W), torch.float32)
+        for t in (disp, conf) if want_conf else (disp,):
+            if tuple(t.shape) != (n, H, W) or not t.is_contiguous():
+                raise ValueError("disp / conf must be contiguous [z1 - z0, H, W]")
+        self._stream()
+        _lib.check(self.L.mvs_ncc_wta_range_d(self.ctx, W, H, _ptr(l8), _ptr(box), cam.desc(), K, z0, z1,
+                                              _ptr(disp), _ptr(conf) if want_conf else None),
+                   "mvs_ncc_wta_range_d")
+        return disp, conf
+
     def levels_dev(self, cam: CameraArray) -> torch.Tensor:
         key = cam.levels.tobytes()
         t = self._levels_dev.get(key)

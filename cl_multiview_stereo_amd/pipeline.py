@@ -87,10 +87,10 @@ class PixelSweep:
         else:
             V, H, W = l8.shape
             box = self.e.box_stats_views(l8, self.K, views, self.e.empty((2, V, H + (H & 1), W, 2), torch.int32))
+        if self.fused:  # every reference view of the call, runs of views per launch
+            self.e.ncc_wta_range(l8, box, self.cam, z0, z1, self.K, disp=disp, conf=conf)
+            return disp, conf
         for i, z in enumerate(range(z0, z1)):
-            if self.fused:
-                self.e.ncc_wta(l8, box, self.cam, z, self.K, disp=disp[i], conf=conf[i])
-                continue
             self.e.ncc_volume(l8, box, self.cam, z, self.K, out=self.vol)
             self.e.wta(self.vol, self.levels, disp=disp[i], conf=conf[i])
         return disp, conf

@@ -150,6 +150,12 @@ int mvs_wta_d(mvs_ctx* ctx, int W, int H, int D, const float* vol, const float* 
  * conf may be NULL. */
 int mvs_ncc_wta_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
                   int K, int z, float* disp, float* conf);
+/* mvs_ncc_wta_d for reference views [z0, z1) into disp/conf [z1 - z0][H][W]:
+ * runs of views that share a sweep variant go in one launch (bit-identical to
+ * one mvs_ncc_wta_d per view; clPhotoConsistency enqueues one sweep per
+ * reference view, photo_consistency.cpp:133). */
+int mvs_ncc_wta_range_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
+                        int K, int z0, int z1, float* disp, float* conf);
 /* Tuning / test hook: the NCC sweep variant this context tries first (0 =
  * automatic): waves per workgroup 4|8, levels per wave 1|2|4 (8 waves: 4),
  * minimum LDS band width 128|192|256 columns, general_rows 1 = the kernel

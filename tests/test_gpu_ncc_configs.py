@@ -187,3 +187,47 @@ def test_every_ncc_variant(eng, K, geom):
     # K = 5 horizontal bands start on a row pair (R + tymax even); K = 7 (R = 3)
     # and fractional vertical shifts start on odd rows
     assert evens == ({0, 1} if geom == "horizontal" and K == 5 else {0})
+
+
+@pytest.mark.parametrize("case", ["c2_like", "c4_like", "c5_like", "frac_vertical", "forced"])
+def test_ncc_wta_range(eng, case):
+    """mvs_ncc_wta_range_d: runs of reference views per launch (one kernel
+    boundary per run, up to 8 views, the run's widest band stride and parity)
+    equal the per-view fused sweep and the oracle, bit for bit -- views with
+    different band widths (C2: 128 vs 192), different variants inside one call
+    (C4: 2- and 1-level-per-wave runs), more views than one launch holds, a
+    sub-range, and a forced variant."""
+    K, z0, z1 = 5, None, None
+    if case == "c2_like":
+        aw, ah, W, H, dmax, nh, nv, knn, bl = 5, 1, 200, 40, 127, 4, 0, None, 1.0
+    elif case == "c4_like":
+        aw, ah, W, H, dmax, nh, nv, knn, bl = 8, 4, 200, 48, 127, 0, 0, 5, 1.0
+    elif case == "c5_like":
+        aw, ah, W, H, dmax, nh, nv, knn, bl, K = 5, 1, 300, 30, 100, 4, 0, None, 1.0, 7
+        z0, z1 = 1, 4
+    elif case == "frac_vertical":
+        aw, ah, W, H, dmax, nh, nv, knn, bl = 3, 3, 96, 60, 20, 1, 1, None, 1.0359
+    else:
+        aw, ah, W, H, dmax, nh, nv, knn, bl = 4, 2, 120, 40, 39, 1, 1, None, 1.0
+        eng.set_ncc_variant(4, 2, 192, False)
+    V = aw * ah
+    z0 = 0 if z0 is None else z0
+    z1 = V if z1 is None else z1
+    stack, _ = synth.make_stack(W, H, aw, ah, 0, dmax, bl, 0x5EED + 9)
+    cam = _array(aw, ah, 0, dmax, nh=nh, nv=nv, knn=knn, bl=bl)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    box = eng.box_stats(l8, K)
+    rd, rc = eng.ncc_wta_range(l8, box, cam, z0, z1, K)
+    l8h = l8.cpu().numpy()
+    for i, z in enumerate(range(z0, z1)):
+        fd, fc = eng.ncc_wta(l8, box, cam, z, K)
+        same(rd[i], fd, f"range vs per-view disp z{z}")
+        same(rc[i], fc, f"range vs per-view conf z{z}")
+        if i % 3 == 0:
+            want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, bl, K, z)
+            od, oc = orc.wta(want, cam.levels)
+            same(rd[i], od, f"range vs oracle disp z{z}")
+            same(rc[i], oc, f"range vs oracle conf z{z}")
+    # no confidence requested
+    nd, _ = eng.ncc_wta_range(l8, box, cam, z0, z1, K, want_conf=False)
+    same(nd, rd, "range without confidence")

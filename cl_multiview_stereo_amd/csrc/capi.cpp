@@ -268,7 +268,7 @@ int mvs_sweep_spixl_d(mvs_ctx* c, int W, int H, int S, const float* lab, float* 
   if (!c || !lab || !spixl || !rep || S <= 0 || bad_dims(W, H)) return mvs::arg_fail("mvs_sweep_spixl_d: bad arguments");
   RC(upload_meta(c, a));
   if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_sweep_spixl_d: bad view range");
-  return mvs::launch_sweep_spixl(c->stream, a->view_count, W, H, S, lab, spixl, rep, c->d_levels, a->num_levels,
+  return mvs::launch_sweep_spixl(c, a->view_count, W, H, S, lab, spixl, rep, c->d_levels, a->num_levels,
                                  c->d_vs, c->d_sn, a->array_width, a->bl_ratio, z0, z1);
 }
 

@@ -80,7 +80,7 @@ int launch_suppress(hipStream_t s, const uint32_t* in, uint32_t* out, int V, int
 
 int launch_boundary(hipStream_t s, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
                     uint8_t* rep);
-int launch_sweep_spixl(hipStream_t s, int V, int W, int H, int S, const float* lab, float* spixl,
+int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* lab, float* spixl,
                        const uint8_t* rep, const float* levels, int D, const int* vs, const int* sn, int aw,
                        float bl, int z0, int z1);
 int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,

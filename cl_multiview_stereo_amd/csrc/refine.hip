@@ -318,53 +318,87 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
   return finish_consistency(cons, vc);
 }
 
-// compute_consistency's sums for ONE neighbour view k (samples in order,
-// each view's sums start at 0 as in the reference): {num, vis_w, occ_w,
-// visibility, visible}.  Same arithmetic as comp_consistency.
-__device__ void view_sums(const PCtx& p, float d, float nx, float ny, float nz, int k, float* o) {
+// compute_consistency's per-sample terms dealt over a candidate's 8 lanes
+// (k_propagate's lane-parallel phase): task = 9 * view slot + sample; lane r takes tasks
+// r, r + 8, ... -- ceil(9 nv / 8) samples per lane instead of one view's 9, so
+// a corner view (3 neighbours) keeps all 8 lanes busy.  The tasks run in
+// batches of 3 (the label gathers of a batch issued before its record
+// gathers) with a wave-uniform trip count ceil(ceil(9 nv / 8) / 3): 2 batches
+// for nv <= 5, 3 for nv = 8 -- a fixed, predicated 9-task loop (the first
+// form of this change) executed all 9 task slots for every view count and
+// was 2 % slower than one view per lane.  Per task the view's camera offsets
+// and the sample's offsets come from per-wave LDS tables; each sample's
+// (t_vis, t_col) and (ok, wv) go to LDS, and view_sum adds a view's 9 samples
+// in order (each view's sums start at 0, as in the reference).  Same
+// arithmetic as comp_consistency, bit for bit.
+__device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, float ny, float nz, int r, int nv,
+                                           const int2* toff, const float4* tview, float2* samp, uint8_t* sflg) {
   const RArgs& c = p.c;
   const long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
-  const int camx = p.z % c.aw, camy = p.z / c.aw;
   const int cxi = (int)p.cx, cyi = (int)p.cy;
-  const int view = p.vs[c.V * p.z + k];
-  const float fdx = (float)(view % c.aw - camx), fdy = (float)(view / c.aw - camy);
-  const uint32_t* lv = p.labels + P * view;
   const float rnz = 1.0f / nz;
-  int xp[9], yp[9];
-  bool ok[9];
-  uint32_t ip[9];
-  float di[9];
+  const int ntask = 9 * nv;
+  const int nb = ((ntask + 7) / 8 + 2) / 3;  // batches of 3 tasks per lane (uniform)
+  for (int b = 0; b < nb; b++) {
+    int xp[3], yp[3], vw[3];
+    bool ok[3];
+    uint32_t ip[3];
+    float di[3];
 #pragma unroll
-  for (int s = 0; s < 9; s++) {
-    const float sxf = (float)(cxi + p.smp[s] * (s / 3 - 1));
-    const float syf = (float)(cyi + p.smp[s] * (s % 3 - 1));
-    di[s] = plane_at_r(nx, ny, nz, rnz, p.cx, p.cy, d, sxf, syf);
-    xp[s] = (int)(sxf - roundf(di[s] * fdx));
-    yp[s] = (int)(syf - roundf((c.bl * di[s]) * fdy));
-    ok[s] = xp[s] >= 0 && yp[s] >= 0 && xp[s] < c.W && yp[s] < c.H;
-    ip[s] = lv[ok[s] ? (long)c.W * yp[s] + xp[s] : 0];
+    for (int i = 0; i < 3; i++) {
+      const int tk = r + 8 * (3 * b + i);
+      xp[i] = yp[i] = vw[i] = 0;
+      ok[i] = false;
+      ip[i] = 0;
+      di[i] = 0.0f;
+      if (tk < ntask) {
+        const int k = tk / 9, sm = tk - 9 * k;
+        const int2 o = toff[sm];
+        const float4 tv = tview[k];
+        const int view = __float_as_int(tv.x);
+        const float sxf = (float)(cxi + o.x), syf = (float)(cyi + o.y);
+        di[i] = plane_at_r(nx, ny, nz, rnz, p.cx, p.cy, d, sxf, syf);
+        xp[i] = (int)(sxf - roundf(di[i] * tv.y));
+        yp[i] = (int)(syf - roundf((c.bl * di[i]) * tv.z));
+        ok[i] = xp[i] >= 0 && yp[i] >= 0 && xp[i] < c.W && yp[i] < c.H;
+        ip[i] = p.labels[P * view + (ok[i] ? (long)c.W * yp[i] + xp[i] : 0)];
+        vw[i] = view;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const int tk = r + 8 * (3 * b + i);
+      if (tk >= ntask) continue;
+      const long q = M * vw[i] + ip[i];
+      const float4 sa = *(const float4*)(p.spixl + 8 * q);
+      const float2 sb = *(const float2*)(p.spixl + 8 * q + 4);
+      const float* sq = p.st + 6 * q;
+      const float2 t0 = *(const float2*)(sq);
+      const float2 t1 = *(const float2*)(sq + 2);
+      const float2 t2 = *(const float2*)(sq + 4);
+      const float dip = plane_at(t1.y, t2.x, t2.y, sa.y, sa.z, t0.x, (float)xp[i], (float)yp[i]);
+      float diff = dip - di[i];
+      const bool wv = fabsf(diff) < c.fuse;
+      const float t_vis = (wv ? 1.0f : 0.0f) * expf_neg_sq(diff, c.alpha);
+      diff = mvs_distance3(sa.w, sb.x, sb.y, p.col[0], p.col[1], p.col[2]);
+      samp[tk] = make_float2(t_vis, expf_neg_sq(diff, c.gamma));
+      sflg[tk] = (uint8_t)((ok[i] ? 1 : 0) | (wv ? 2 : 0));
+    }
   }
+}
+// one view's {num, vis_w, occ_w, visibility, visible} from its 9 task results, samples in order
+__device__ __forceinline__ void view_sum(const float2* samp, const uint8_t* sflg, float* o) {
   float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
 #pragma unroll
   for (int s = 0; s < 9; s++) {
-    const long q = M * view + ip[s];
-    const float4 sa = *(const float4*)(p.spixl + 8 * q);
-    const float2 sb = *(const float2*)(p.spixl + 8 * q + 4);
-    const float* sq = p.st + 6 * q;
-    const float2 t0 = *(const float2*)(sq);
-    const float2 t1 = *(const float2*)(sq + 2);
-    const float2 t2 = *(const float2*)(sq + 4);
-    float dip = plane_at(t1.y, t2.x, t2.y, sa.y, sa.z, t0.x, (float)xp[s], (float)yp[s]);
-    float diff = dip - di[s];
-    const float wv = fabsf(diff) < c.fuse ? 1.0f : 0.0f;
-    const float t_vis = wv * expf_neg_sq(diff, c.alpha);
-    diff = mvs_distance3(sa.w, sb.x, sb.y, p.col[0], p.col[1], p.col[2]);
-    const float t_col = expf_neg_sq(diff, c.gamma);
-    if (ok[s]) {
-      visible = visible + t_vis;
+    const int f = sflg[s];
+    if (f & 1) {
+      const float2 v = samp[s];
+      const float wv = (f & 2) ? 1.0f : 0.0f;
+      visible = visible + v.x;
       vis_w = vis_w + wv;
       occ_w = occ_w + (1.0f - wv);
-      visibility = visibility + t_col;
+      visibility = visibility + v.y;
       num = num + 1.0f;
     }
   }
@@ -491,7 +525,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     __shared__ float s_prod[4][8][64];
     __shared__ float s_view[4][8][kTriViews][5];
     __shared__ int s_slot[4][64];
+    __shared__ float2 s_samp[4][8][9 * kTriViews];   // view_tasks results per candidate
+    __shared__ uint8_t s_sflg[4][8][9 * kTriViews];
+    __shared__ int2 s_toff[4][9];                     // sample offsets of this superpixel
+    __shared__ float4 s_tview[4][kTriViews];          // {view, dx, dy} of each neighbour slot
     const int w = threadIdx.x >> 6;
+    if (lane < 9) {  // samples_of: extents 0..3, the centre, extents 4..7
+      const int e = lane == 4 ? 0 : (int)rep[8 * idx + (lane < 4 ? lane : lane - 1)];
+      s_toff[w][lane] = make_int2(e * (lane / 3 - 1), e * (lane % 3 - 1));
+    }
+    if (lane < nv) {
+      const int view = vs[c.V * z + lane];
+      s_tview[w][lane] = make_float4(__int_as_float(view), (float)(view % c.aw - z % c.aw),
+                                     (float)(view / c.aw - z / c.aw), 0.0f);
+    }
     const int t = lane >> 3, r = lane & 7;
     const long qk = lane < nslot ? cand(lane) : -1;
     const unsigned long long vmask = __ballot(qk >= 0);
@@ -558,8 +605,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
           s_prod[w][t][l] = simi * expf_neg_sq(diff, c.alpha);
         }
       }
+      if (ok) view_tasks(p, pd, n0, n1, n2, r, nv, s_toff[w], s_tview[w], s_samp[w][t], s_sflg[w][t]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       for (int k = r; k < nv; k += 8)
-        if (ok) view_sums(p, pd, n0, n1, n2, k, s_view[w][t][k]);
+        if (ok) view_sum(s_samp[w][t] + 9 * k, s_sflg[w][t] + 9 * k, s_view[w][t][k]);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

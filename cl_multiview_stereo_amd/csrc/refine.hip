@@ -338,15 +338,16 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, flo
   const int cxi = (int)p.cx, cyi = (int)p.cy;
   const float rnz = 1.0f / nz;
   const int ntask = 9 * nv;
-  const int nb = ((ntask + 7) / 8 + 2) / 3;  // batches of 3 tasks per lane (uniform)
+  constexpr int TB = 3;  // tasks per batch (2 measured the same)
+  const int nb = ((ntask + 7) / 8 + TB - 1) / TB;  // batches per lane (uniform)
   for (int b = 0; b < nb; b++) {
-    int xp[3], yp[3], vw[3];
-    bool ok[3];
-    uint32_t ip[3];
-    float di[3];
+    int xp[TB], yp[TB], vw[TB];
+    bool ok[TB];
+    uint32_t ip[TB];
+    float di[TB];
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
-      const int tk = r + 8 * (3 * b + i);
+    for (int i = 0; i < TB; i++) {
+      const int tk = r + 8 * (TB * b + i);
       xp[i] = yp[i] = vw[i] = 0;
       ok[i] = false;
       ip[i] = 0;
@@ -366,8 +367,8 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, flo
       }
     }
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
-      const int tk = r + 8 * (3 * b + i);
+    for (int i = 0; i < TB; i++) {
+      const int tk = r + 8 * (TB * b + i);
       if (tk >= ntask) continue;
       const long q = M * vw[i] + ip[i];
       const float4 sa = *(const float4*)(p.spixl + 8 * q);
@@ -386,7 +387,11 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, flo
     }
   }
 }
-// one view's {num, vis_w, occ_w, visibility, visible} from its 9 task results, samples in order
+// one view's sums {num, vis_w, occ_w, visibility, visible} from its 9 task
+// results, samples in order, finished into what compute_consistency adds for
+// the view: o = {num, ((vis_w/num)*(visibility/vis_w))*(visible/vis_w) (0 if
+// vis_w == 0), vis_w > 0, occ_w > 0} -- the three divides run here, one lane
+// per view, instead of serially on the candidate's lane 8t
 __device__ __forceinline__ void view_sum(const float2* samp, const uint8_t* sflg, float* o) {
   float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
 #pragma unroll
@@ -402,7 +407,10 @@ __device__ __forceinline__ void view_sum(const float2* samp, const uint8_t* sflg
       num = num + 1.0f;
     }
   }
-  o[0] = num; o[1] = vis_w; o[2] = occ_w; o[3] = visibility; o[4] = visible;
+  o[0] = num;
+  o[1] = vis_w > 0 ? ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w) : 0.0f;
+  o[2] = vis_w > 0 ? 1.0f : 0.0f;
+  o[3] = occ_w > 0 ? 1.0f : 0.0f;
 }
 
 // One WAVE per superpixel.  The reference evaluates its candidate planes one
@@ -529,7 +537,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     __shared__ uint8_t s_sflg[4][8][9 * kTriViews];
     __shared__ int2 s_toff[4][9];                     // sample offsets of this superpixel
     __shared__ float4 s_tview[4][kTriViews];          // {view, dx, dy} of each neighbour slot
+    __shared__ int s_term[4][64];                     // the valid smoothness terms, in term order
     const int w = threadIdx.x >> 6;
+    // compacted smoothness terms: the far terms that leave the superpixel map
+    // (most of them at S = 8 in the first iterations: 61 terms, ~8 valid) take
+    // no loop trips; products stored and summed by compacted index, i.e. in the
+    // reference's term order over the valid terms
+    const int nvt = __popcll(t_valid);
+    if ((t_valid >> lane) & 1ull) s_term[w][__popcll(t_valid & ((1ull << lane) - 1ull))] = lane;
     if (lane < 9) {  // samples_of: extents 0..3, the centre, extents 4..7
       const int e = lane == 4 ? 0 : (int)rep[8 * idx + (lane < 4 ? lane : lane - 1)];
       s_toff[w][lane] = make_int2(e * (lane / 3 - 1), e * (lane % 3 - 1));
@@ -594,15 +609,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
       }
       const float rn2 = 1.0f / n2;
-      // smoothness products; uniform trip count so every lane takes part in the shuffles
-      for (int i = 0; i < (nterm + 7) / 8; i++) {
-        const int l = r + 8 * i;
-        const int ls = l < 64 ? l : 0;
+      // smoothness products over the compacted valid terms; uniform trip count so
+      // every lane takes part in the shuffles
+      for (int i = 0; i < (nvt + 7) / 8; i++) {
+        const int j = r + 8 * i;
+        const int ls = j < nvt ? s_term[w][j] : 0;
         const float simi = __shfl(t_simi, ls), sx = __shfl(t_sx, ls), sy = __shfl(t_sy, ls), sd = __shfl(t_sd, ls);
-        if (ok && l < nterm && ((t_valid >> l) & 1ull)) {
+        if (ok && j < nvt) {
           const float di = plane_at_r(n0, n1, n2, rn2, p.cx, p.cy, pd, sx, sy);
           const float diff = di - sd;
-          s_prod[w][t][l] = simi * expf_neg_sq(diff, c.alpha);
+          s_prod[w][t][j] = simi * expf_neg_sq(diff, c.alpha);
         }
       }
       if (ok) view_tasks(p, pd, n0, n1, n2, r, nv, s_toff[w], s_tview[w], s_samp[w][t], s_sflg[w][t]);
@@ -617,18 +633,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       float sm1 = 0.f, cs1 = 0.f;
       if (ok && r == 0) {
         float sm = 0.0f;
-        for (int l = 0; l < nterm; l++)
-          if ((t_valid >> l) & 1ull) sm = sm + s_prod[w][t][l];
+        for (int j = 0; j < nvt; j++) sm = sm + s_prod[w][t][j];
         sm1 = wn > 0 ? sm / wn : 0.000001f;
         float cons = 0.0f;
         int vc = 0;
         for (int k = 0; k < nv; k++) {
           const float* o = s_view[w][t][k];
-          const float num = o[0], vis_w = o[1], occ_w = o[2], visibility = o[3], visible = o[4];
-          if (num > 0) {
+          if (o[0] > 0) {  // num > 0
             vc++;
-            if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
-            if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)p.fl.y);
+            if (o[2] != 0.0f) cons = cons + o[1];                               // vis_w > 0
+            if (o[3] != 0.0f) cons = (float)((double)cons + 0.5 * (double)p.fl.y);  // occ_w > 0
           }
         }
         cs1 = finish_consistency(cons, vc);

@@ -331,15 +331,16 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
 // (t_vis, t_col) and (ok, wv) go to LDS, and view_sum adds a view's 9 samples
 // in order (each view's sums start at 0, as in the reference).  Same
 // arithmetic as comp_consistency, bit for bit.
-__device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, float ny, float nz, int r, int nv,
-                                           const int2* toff, const float4* tview, float2* samp, uint8_t* sflg) {
+__device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, float ny, float nz, int r, int L,
+                                           int nv, const int2* toff, const float4* tview, float2* samp,
+                                           uint8_t* sflg) {
   const RArgs& c = p.c;
   const long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
   const int cxi = (int)p.cx, cyi = (int)p.cy;
   const float rnz = 1.0f / nz;
   const int ntask = 9 * nv;
   constexpr int TB = 3;  // tasks per batch (2 measured the same)
-  const int nb = ((ntask + 7) / 8 + TB - 1) / TB;  // batches per lane (uniform)
+  const int nb = ((ntask + L - 1) / L + TB - 1) / TB;  // batches per lane (uniform)
   for (int b = 0; b < nb; b++) {
     int xp[TB], yp[TB], vw[TB];
     bool ok[TB];
@@ -347,7 +348,7 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, flo
     float di[TB];
 #pragma unroll
     for (int i = 0; i < TB; i++) {
-      const int tk = r + 8 * (TB * b + i);
+      const int tk = r + L * (TB * b + i);
       xp[i] = yp[i] = vw[i] = 0;
       ok[i] = false;
       ip[i] = 0;
@@ -368,7 +369,7 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, flo
     }
 #pragma unroll
     for (int i = 0; i < TB; i++) {
-      const int tk = r + 8 * (TB * b + i);
+      const int tk = r + L * (TB * b + i);
       if (tk >= ntask) continue;
       const long q = M * vw[i] + ip[i];
       const float4 sa = *(const float4*)(p.spixl + 8 * q);
@@ -520,7 +521,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const int nv = sn[z];
   if (fast_sm && nv <= kTriViews) {
     // Lane-parallel evaluation in groups of 8 candidates: lane 8t + r works
-    // for candidate t of the group.  The smoothness products simi_l * exp(...)
+    // for candidate t of the group (L lanes per candidate in general: 8, or
+    // more for a partial last group, see below).  The smoothness products simi_l * exp(...)
     // are computed by lanes r = l mod 8 into LDS and summed in term order by
     // lane 8t; each view's consistency sums (9 samples in order) by lane
     // r = view mod 8, combined in view order by lane 8t -- every float sum in
@@ -554,7 +556,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       s_tview[w][lane] = make_float4(__int_as_float(view), (float)(view % c.aw - z % c.aw),
                                      (float)(view / c.aw - z / c.aw), 0.0f);
     }
-    const int t = lane >> 3, r = lane & 7;
     const long qk = lane < nslot ? cand(lane) : -1;
     const unsigned long long vmask = __ballot(qk >= 0);
     if (qk >= 0) s_slot[w][__popcll(vmask & ((1ull << lane) - 1ull))] = lane;
@@ -567,6 +568,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int nby[8] = {y, y - 1, y - 1, y - 1, y, y + 1, y + 1, y + 1};
     for (int gi = 0; gi <= ngrp; gi++) {
       const bool tri = gi == ngrp;
+      // lanes per candidate: 8, or 16 / 32 / 64 for a plane group of at most
+      // 4 / 2 / 1 candidates (the last group: at S = 8 most iterations have 9-13
+      // valid candidates, so a full group of 8 and a partial one)
+      const int ncg = tri ? 8 : min(8, nvalid - 8 * gi);
+      const int lg = ncg > 4 ? 3 : ncg > 2 ? 4 : ncg > 1 ? 5 : 6, L = 1 << lg;
+      const int t = lane >> lg, r = lane & (L - 1);
       bool ok;
       float pd = cur.d, n0 = 0.f, n1 = 0.f, n2 = 1.f, ksimi = 0.f;
       if (!tri) {  // plane candidate: update(), clcode.cl:1635-1673, minus the accept test
@@ -611,8 +618,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       const float rn2 = 1.0f / n2;
       // smoothness products over the compacted valid terms; uniform trip count so
       // every lane takes part in the shuffles
-      for (int i = 0; i < (nvt + 7) / 8; i++) {
-        const int j = r + 8 * i;
+      for (int i = 0; i < (nvt + L - 1) >> lg; i++) {
+        const int j = r + L * i;
         const int ls = j < nvt ? s_term[w][j] : 0;
         const float simi = __shfl(t_simi, ls), sx = __shfl(t_sx, ls), sy = __shfl(t_sy, ls), sd = __shfl(t_sd, ls);
         if (ok && j < nvt) {
@@ -621,11 +628,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
           s_prod[w][t][j] = simi * expf_neg_sq(diff, c.alpha);
         }
       }
-      if (ok) view_tasks(p, pd, n0, n1, n2, r, nv, s_toff[w], s_tview[w], s_samp[w][t], s_sflg[w][t]);
+      if (ok) view_tasks(p, pd, n0, n1, n2, r, L, nv, s_toff[w], s_tview[w], s_samp[w][t], s_sflg[w][t]);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int k = r; k < nv; k += 8)
+      for (int k = r; k < nv; k += L)
         if (ok) view_sum(s_samp[w][t] + 9 * k, s_sflg[w][t] + 9 * k, s_view[w][t][k]);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -652,17 +659,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const unsigned long long valid = __ballot(ok && r == 0);
-      for (int l = 0; l < 8; l++) {  // accept tests in candidate order
-        if (!((valid >> (8 * l)) & 1ull)) continue;
-        const float ksm = bcast(sm1, 8 * l), kcs = bcast(cs1, 8 * l);
+      for (int l = 0; l < (64 >> lg); l++) {  // accept tests in candidate order
+        if (!((valid >> (L * l)) & 1ull)) continue;
+        const float ksm = bcast(sm1, L * l), kcs = bcast(cs1, L * l);
         if (!tri) {
-          const float ksi = bcast(ksimi, 8 * l);
+          const float ksi = bcast(ksimi, L * l);
           if ((iter < 4 && ksm * ksi > cur.sm) || kcs * ksm > cur.sm * cur.cs) {
-            cur.d = bcast(pd, 8 * l); cur.sm = ksm; cur.cs = kcs;
-            cur.nx = bcast(n0, 8 * l); cur.ny = bcast(n1, 8 * l); cur.nz = bcast(n2, 8 * l);
+            cur.d = bcast(pd, L * l); cur.sm = ksm; cur.cs = kcs;
+            cur.nx = bcast(n0, L * l); cur.ny = bcast(n1, L * l); cur.nz = bcast(n2, L * l);
           }
         } else if ((iter < 4 && ksm > cur.sm) || ksm * kcs > cur.sm * cur.cs) {
-          cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, 8 * l); cur.ny = bcast(n1, 8 * l); cur.nz = bcast(n2, 8 * l);
+          cur.sm = ksm; cur.cs = kcs; cur.nx = bcast(n0, L * l); cur.ny = bcast(n1, L * l); cur.nz = bcast(n2, L * l);
         }
       }
     }

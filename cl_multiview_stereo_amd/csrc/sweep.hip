@@ -79,19 +79,23 @@ struct SweepArgs {
 // strict-< scan over levels in index order -- through LDS.  LPS = 32 (D <= 32,
 // e.g. the reference's default 31 levels): two superpixels per wave, one per
 // 32-lane half, so no lane idles past the last level.
-// Vertical neighbours (same camera column): lane = level puts 64 levels' taps
-// on 64 different rows -- 64 cache lines per gather instruction, 16 B used of
-// each 128.  labT (optional) holds those views transposed, [slot][x][y]
-// (tslot[view] >= 0), so the levels' taps of one column are contiguous.
-// Measured at C4 (8x4 array, 5 nearest neighbours, all 32 views): TCC_MISS
-// 271 M per launch against 175 M hits, 4.66 ms.
+// Vertical and diagonal neighbours: lane = level puts 64 levels' taps on 64
+// different rows -- 64 cache lines per gather instruction, 16 B used of each
+// 128 (measured at C4, 8x4 array, 5 nearest neighbours, all 32 views:
+// TCC_MISS 271 M per launch against 175 M hits, 4.66 ms).  labT (optional)
+// holds such neighbour views re-laid so that consecutive levels' taps are
+// consecutive elements: slot tslot[4 * view + kind] (stride tstride elements)
+// of kind 1 (same camera column: transposed, element (x, y) at x H + y),
+// 2 (dx == dy: sheared, at (x - y + H - 1) H + y) or 3 (dx == -dy: at
+// (x + y) H + y).  With bl != 1 the diagonal shifts drift apart by a row
+// every 1/|bl - 1| levels: still a few lines per instruction instead of 64.
 template <int LPS>
 __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ lab, float* __restrict__ spixl,
                                                      const uint8_t* __restrict__ rep,
                                                      const float* __restrict__ levels, const int* __restrict__ vs,
                                                      const int* __restrict__ sn, SweepArgs a, int wps,
                                                      const float4* __restrict__ labT,
-                                                     const int* __restrict__ tslot) {
+                                                     const int* __restrict__ tslot, long tstride) {
   __shared__ float4 refc[8][25];
   __shared__ int2 refxy[8][25];
   __shared__ float wbest[4];
@@ -140,9 +144,14 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       int vx = view % a.aw, vy = view / a.aw;
       float fdx = d * (float)(vx - rx);
       float fdy = (a.bl * d) * (float)(vy - ry);
-      const int ts = (labT && vx == rx) ? tslot[view] : -1;
-      const float4* labv = ts >= 0 ? labT + (long)ts * P : lab + (long)view * P;
-      const int sxs = ts >= 0 ? a.H : 1, sys = ts >= 0 ? 1 : a.W;  // element strides of x and y
+      const int ddx = vx - rx, ddy = vy - ry;
+      const int kind = !labT ? 0 : ddx == 0 ? 1 : ddx == ddy ? 2 : ddx == -ddy ? 3 : 0;
+      const int ts = kind ? tslot[4 * view + kind] : -1;
+      const float4* labv = ts >= 0 ? labT + (long)ts * tstride : lab + (long)view * P;
+      // element index = off + x sxs + y sys in the view's layout
+      const int sxs = ts < 0 ? 1 : a.H;
+      const int sys = ts < 0 ? a.W : kind == 1 ? 1 : kind == 2 ? 1 - a.H : a.H + 1;
+      const int off = ts >= 0 && kind == 2 ? (a.H - 1) * a.H : 0;
       float val = 0.0f;
       // branch-free taps: every load is issued (out-of-image taps read pixel 0
       // and are dropped by the select), so the 25 gathers of a neighbour are
@@ -153,7 +162,7 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
         int xp = (int)((float)r.x - fdx);
         int yp = (int)((float)r.y - fdy);
         const bool in = r.x >= 0 && r.y >= 0 && xp >= 0 && yp >= 0 && r.x < a.W && r.y < a.H && xp < a.W && yp < a.H;
-        const float4 B = labv[in ? yp * sys + xp * sxs : 0];
+        const float4 B = labv[in ? off + yp * sys + xp * sxs : 0];
         const float4 A = refc[slot][t];
         float ad = fabsf(A.x - B.x) + fabsf(A.y - B.y);
         ad = ad + fabsf(A.z - B.z);
@@ -682,9 +691,12 @@ int launch_boundary(hipStream_t s, int V, int W, int H, int S, const float* spix
   return 0;
 }
 
-// lab view `view` -> out [x][y] (32 x 32 tiles through LDS)
-__global__ __launch_bounds__(256) void k_transpose_lab(const float4* __restrict__ lab, int W, int H, int view,
-                                                       float4* __restrict__ out) {
+// lab view `view` re-laid for the superpixel sweep (see k_sweep_spixl): KIND 1
+// transposed, 2 / 3 sheared along x - y / x + y; 32 x 32 tiles through LDS,
+// written along the output's contiguous direction (columns, or diagonals)
+template <int KIND>
+__global__ __launch_bounds__(256) void k_relayout_lab(const float4* __restrict__ lab, int W, int H, int view,
+                                                      float4* __restrict__ out) {
   __shared__ float4 t[32][33];
   const int x0 = blockIdx.x * 32, y0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const float4* src = lab + (long)view * W * H;
@@ -694,10 +706,21 @@ __global__ __launch_bounds__(256) void k_transpose_lab(const float4* __restrict_
     if (x < W && y < H) t[ty + 8 * k][tx] = src[(long)y * W + x];
   }
   __syncthreads();
+  if (KIND == 1) {
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int x = x0 + ty + 8 * k, y = y0 + tx;
-    if (x < W && y < H) out[(long)x * H + y] = t[tx][ty + 8 * k];
+    for (int k = 0; k < 4; k++) {
+      const int x = x0 + ty + 8 * k, y = y0 + tx;
+      if (x < W && y < H) out[(long)x * H + y] = t[tx][ty + 8 * k];
+    }
+    return;
+  }
+  // the tile's 63 diagonals, 8 per pass; lane tx = the row within the tile
+  for (int d0 = 0; d0 < 63; d0 += 8) {
+    const int dd = d0 + ty, yl = tx;
+    const int xl = KIND == 2 ? yl + dd - 31 : dd - yl;
+    const int x = x0 + xl, y = y0 + yl;
+    if (dd < 63 && xl >= 0 && xl < 32 && x < W && y < H)
+      out[KIND == 2 ? (long)(x - y + H - 1) * H + y : (long)(x + y) * H + y] = t[yl][xl];
   }
 }
 
@@ -714,37 +737,51 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
   const int spb = half ? 8 : 4 / wps;
   SweepArgs a{V, W, H, mw, mh, D, aw, z0, bl};
   const long nb = (M + spb - 1) / spb;
-  // the vertical neighbours (same camera column) of the references, transposed
-  // into the context scratch; MVS_SWEEP_TRANSPOSE=0 (read per call) keeps the
-  // row-major gathers (A/B)
+  // the vertical and diagonal neighbours of the references, re-laid into the
+  // context scratch; MVS_SWEEP_TRANSPOSE (read per call) = 0: row-major
+  // gathers only, 1: vertical neighbours only, 2 (default): both (A/B)
   const float4* labT = nullptr;
   const int* tslot = nullptr;
+  const long tstride = (long)(W + H - 1) * H;  // elements per re-laid slot (the sheared layouts' size)
   const char* te = getenv("MVS_SWEEP_TRANSPOSE");
-  if (!(te && te[0] == '0')) {
-    std::vector<int32_t> slot(V, -1);
+  const int tmode = te ? atoi(te) : 2;
+  if (tmode > 0) {
+    std::vector<int32_t> slot(4 * (size_t)V, -1);
     int nt = 0;
     for (int z = z0; z < z1; z++)
       for (int k = 0; k < ctx->h_sn[z]; k++) {
         const int v = ctx->h_vs[(size_t)V * z + k];
-        if (v >= 0 && v < V && v % aw == z % aw && slot[v] < 0) slot[v] = nt++;
+        if (v < 0 || v >= V) continue;
+        const int dx = v % aw - z % aw, dy = v / aw - z / aw;
+        const int kind = dx == 0 ? 1 : tmode < 2 ? 0 : dx == dy ? 2 : dx == -dy ? 3 : 0;
+        if (kind && slot[4 * v + kind] < 0) slot[4 * v + kind] = nt++;
       }
     if (nt > 0) {
       int rc = 0;
-      float4* buf = (float4*)scratch(ctx, (size_t)nt * W * H * sizeof(float4), &rc);
+      float4* buf = (float4*)scratch(ctx, (size_t)nt * tstride * sizeof(float4), &rc);
       if (rc) return rc;
       tslot = plan_upload(ctx, slot, &rc);
       if (rc) return rc;
+      const dim3 tg((W + 31) / 32, (H + 31) / 32);
       for (int v = 0; v < V; v++)
-        if (slot[v] >= 0)
-          hipLaunchKernelGGL(k_transpose_lab, dim3((W + 31) / 32, (H + 31) / 32), dim3(256), 0, s,
-                             (const float4*)lab, W, H, v, buf + (long)slot[v] * W * H);
-      MVS_LAUNCH_CHECK("k_transpose_lab");
+        for (int kind = 1; kind < 4; kind++) {
+          const int sl = slot[4 * v + kind];
+          if (sl < 0) continue;
+          float4* o = buf + (long)sl * tstride;
+          if (kind == 1)
+            hipLaunchKernelGGL(k_relayout_lab<1>, tg, dim3(256), 0, s, (const float4*)lab, W, H, v, o);
+          else if (kind == 2)
+            hipLaunchKernelGGL(k_relayout_lab<2>, tg, dim3(256), 0, s, (const float4*)lab, W, H, v, o);
+          else
+            hipLaunchKernelGGL(k_relayout_lab<3>, tg, dim3(256), 0, s, (const float4*)lab, W, H, v, o);
+        }
+      MVS_LAUNCH_CHECK("k_relayout_lab");
       labT = buf;
     }
   }
   hipLaunchKernelGGL(half ? k_sweep_spixl<32> : k_sweep_spixl<64>, dim3((unsigned)(8 * ((nb + 7) / 8)),
                      (unsigned)(z1 - z0)), dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a, wps,
-                     labT, tslot);
+                     labT, tslot, tstride);
   MVS_LAUNCH_CHECK("k_sweep_spixl");
   return 0;
 }

@@ -236,10 +236,10 @@ def test_ncc_wta_range(eng, case):
 @pytest.mark.parametrize("bl", [1.0, 1.0359])
 def test_sweep_spixl_transposed_vertical(engine, monkeypatch, bl):
     """The superpixel sweep reads vertical neighbours (same camera column) from
-    a transposed copy of their Lab: C4's array (5 nearest neighbours: vertical,
-    horizontal, diagonal) at 128 levels, every reference view, equal to the
-    row-major gathers (MVS_SWEEP_TRANSPOSE=0) and to the oracle; also a view
-    sub-range (a shard's block)."""
+    a transposed copy of their Lab and diagonal ones from sheared copies: C4's
+    array (5 nearest neighbours: vertical, horizontal, diagonal) at 128
+    levels, every reference view, equal to the row-major gathers
+    (MVS_SWEEP_TRANSPOSE=0) and to the oracle; also a view sub-range."""
     aw, ah, W, H, S = 8, 4, 160, 96, 16
     stack, _ = synth.make_stack(W, H, aw, ah, 0, 127, bl, 0x5EED + 11)
     cam = _array(aw, ah, 0, 127, knn=5, bl=bl)
@@ -247,15 +247,17 @@ def test_sweep_spixl_transposed_vertical(engine, monkeypatch, bl):
     sp, lb = engine.slic(lab, S)
     rep = engine.boundary(sp, lb, S)
     out = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "2"):  # row-major only / + transposed vertical / + sheared diagonal
         monkeypatch.setenv("MVS_SWEEP_TRANSPOSE", mode)
         s = sp.clone()
         engine.sweep_spixl(lab, s, rep, cam, S)
         out[mode] = s
     same(out["1"], out["0"], "transposed vs row-major superpixel sweep")
+    same(out["2"], out["0"], "transposed + sheared vs row-major superpixel sweep")
     osp = orc.sweep(lab.cpu().numpy(), sp.cpu().numpy(), rep.cpu().numpy(), cam.levels, cam.view_subset,
                     cam.subset_num, aw, bl, S)
-    same(out["1"][..., 7], osp[..., 7], "transposed superpixel sweep vs oracle")
+    same(out["2"][..., 7], osp[..., 7], "re-laid superpixel sweep vs oracle")
+    monkeypatch.delenv("MVS_SWEEP_TRANSPOSE")
     s = sp.clone()
     engine.sweep_spixl(lab, s, rep, cam, S, 12, 16)
-    same(s[12:16], out["1"][12:16], "view sub-range")
+    same(s[12:16], out["2"][12:16], "view sub-range")

@@ -940,14 +940,25 @@ __global__ void k_remove_incons(const float* __restrict__ proj, const float* __r
 // largest d down, every view holding that d retired together, and the first
 // stable one is the answer: usually one or two stability evaluations per
 // pixel instead of V, i.e. O(V) instead of O(V^2) work at V = 32 (C4).
+// The views' camera offsets from the reference come from an LDS table (the
+// block's reference is uniform), the reprojection rounds with round_ha and
+// the gathers are 32-bit buffer loads (the launcher checks V * P * 4 < 2^31):
+// the per-view integer divisions and 64-bit address arithmetic made the
+// kernel VALU-bound (C3, V = 5: 443 us for 5 references).
 template <int MAXV>
 __global__ __launch_bounds__(256) void k_remove_incons_sel(const float* __restrict__ proj, const float* __restrict__ full,
                                                            int V, int W, int H, int aw, float bl, float fuse, int z0,
                                                            float* __restrict__ out, int y0, long PP) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = y0 + blockIdx.y, r = z0 + blockIdx.z;
+  __shared__ float2 s_off[MAXV];  // (float)(cx - crx), (float)(cy - cry) of view j
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = y0 + blockIdx.y, r = z0 + blockIdx.z;
+  if ((int)threadIdx.x < MAXV)
+    s_off[threadIdx.x] = make_float2((float)((int)threadIdx.x % aw - r % aw), (float)((int)threadIdx.x / aw - r / aw));
+  __syncthreads();
   if (x >= W) return;
-  long P = (long)W * H, p = (long)y * W + x;
-  int crx = r % aw, cry = r / aw;
+  const long P = (long)W * H, p = (long)y * W + x;
+  const unsigned P4 = (unsigned)(P * 4);
+  const float xf = (float)x, yf = (float)y;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)full, 0, 0x7fffffff, 0x00020000);
   float pv[MAXV];
   unsigned long long live = 0ull;  // candidates not yet tried: d != 0
 #pragma unroll
@@ -978,17 +989,21 @@ __global__ __launch_bounds__(256) void k_remove_incons_sel(const float* __restri
     // (stab counts exactly, so this only skips work).  Views go in blocks of
     // 8 whose gathers are all in flight together; the bound is checked
     // between blocks (a few extra views at most, one round trip per block).
+    const float bd = bl * d;
     for (int j0 = 0; j0 < V && stab + (float)(V - j0) >= 0.0f; j0 += 8) {
       float dc[8];
       bool in[8];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int j = j0 + u;
-        const int cx = j % aw, cy = j / aw;
-        const int xx = (int)((float)x - roundf(d * (float)(cx - crx)));
-        const int yy = (int)((float)y - roundf((bl * d) * (float)(cy - cry)));
-        in[u] = j < V && xx >= 0 && yy >= 0 && xx < W && yy < H;
-        dc[u] = in[u] ? full[P * j + (long)W * yy + xx] : 0.0f;
+        const float2 o = s_off[j < MAXV ? j : 0];
+        const int xx = (int)(xf - round_ha(d * o.x));
+        const int yy = (int)(yf - round_ha(bd * o.y));
+        in[u] = j < V && (unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H;
+        // every lane issues its load (a skipped tap reads 0 past the buffer)
+        const int off = in[u] ? (int)((unsigned)j * P4 + (__umul24((unsigned)yy, (unsigned)W) + (unsigned)xx) * 4u)
+                              : 0x7fffffff;
+        dc[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) {
@@ -1666,7 +1681,8 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
     const dim3 gp((W + 255) / 256, NR);
     // few views: one thread per (reference, pixel) keeps more threads in flight
     // (measured at V = 5: 350 vs 395 us); many views: one thread per pixel
-    if (V <= 8)
+    const bool off32 = (long)V * W * H * 4 < (1L << 31);  // 32-bit gather offsets (the sel / q kernels)
+    if (V <= 8 && off32)
       hipLaunchKernelGGL(k_remove_incons_sel<8>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out, ya, PP);
     else if (V <= 16)
       hipLaunchKernelGGL((k_remove_incons_px<16, 8>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, z1,
@@ -1764,7 +1780,7 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
         hipLaunchKernelGGL((k_remove_incons_px<32, 8>), gp, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0,
                            z1, out, ya, PP);
     }
-    else if (V <= 64)
+    else if (V <= 64 && off32)
       hipLaunchKernelGGL(k_remove_incons_sel<64>, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out, ya, PP);
     else
       hipLaunchKernelGGL(k_remove_incons, g, dim3(256), 0, s, proj, full, V, W, H, aw, bl, fuse, z0, out, ya, PP);

@@ -725,12 +725,15 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   const uint2* pk = stats + (long)V * W * (H + (H & 1));
   constexpr int RW = sizeof(NccRec) / 4;
   const long P = (long)W * H;
+  // MVS_NCC_RUN (read per call): views per launch at most (A/B; default kMaxRef)
+  const char* re = getenv("MVS_NCC_RUN");
+  const int maxrun = re ? std::max(1, std::min(kMaxRef, atoi(re))) : kMaxRef;
   for (int i = 0; i < n;) {
     int bwt = ch[i].bwt, pkp = ch[i].plan.pk_pairs, stp = ch[i].plan.st_pairs;
     bool even = ch[i].plan.even;
     size_t cap = ch[i].cap;
     int j = i + 1;
-    while (!vol && j < n && j - i < kMaxRef && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw) {
+    while (!vol && j < n && j - i < maxrun && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw) {
       const int b2 = std::max(bwt, ch[j].bwt);
       const int p2 = std::max(pkp, ch[j].plan.pk_pairs), s2 = std::max(stp, ch[j].plan.st_pairs);
       const size_t c2 = std::min(cap, ch[j].cap);

@@ -331,13 +331,11 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
 // (t_vis, t_col) and (ok, wv) go to LDS, and view_sum adds a view's 9 samples
 // in order (each view's sums start at 0, as in the reference).  Same
 // arithmetic as comp_consistency, bit for bit.
-__device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, float ny, float nz, int r, int L,
-                                           int nv, const int2* toff, const float4* tview, float2* samp,
-                                           uint8_t* sflg) {
+__device__ __forceinline__ void view_tasks(const PCtx& p, int r, int L, int nv, const int2* toff,
+                                           const float4* tview, const float* sdi, float2* samp, uint8_t* sflg) {
   const RArgs& c = p.c;
   const long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
   const int cxi = (int)p.cx, cyi = (int)p.cy;
-  const float rnz = 1.0f / nz;
   const int ntask = 9 * nv;
   constexpr int TB = 3;  // tasks per batch (2 measured the same)
   const int nb = ((ntask + L - 1) / L + TB - 1) / TB;  // batches per lane (uniform)
@@ -359,7 +357,7 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, float d, float nx, flo
         const float4 tv = tview[k];
         const int view = __float_as_int(tv.x);
         const float sxf = (float)(cxi + o.x), syf = (float)(cyi + o.y);
-        di[i] = plane_at_r(nx, ny, nz, rnz, p.cx, p.cy, d, sxf, syf);
+        di[i] = sdi[sm];  // the candidate plane at sample sm (view-independent, computed once)
         xp[i] = (int)(sxf - roundf(di[i] * tv.y));
         yp[i] = (int)(syf - roundf((c.bl * di[i]) * tv.z));
         ok[i] = xp[i] >= 0 && yp[i] >= 0 && xp[i] < c.W && yp[i] < c.H;
@@ -533,13 +531,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // At S = 8 most far candidates leave the map, so one group of 8 neighbour
     // planes keeps all 64 lanes busy instead of 8.
     __shared__ float s_prod[4][8][64];
-    __shared__ float s_view[4][8][kTriViews][5];
+    __shared__ float s_view[4][8][kTriViews][4];
     __shared__ int s_slot[4][64];
     __shared__ float2 s_samp[4][8][9 * kTriViews];   // view_tasks results per candidate
     __shared__ uint8_t s_sflg[4][8][9 * kTriViews];
     __shared__ int2 s_toff[4][9];                     // sample offsets of this superpixel
     __shared__ float4 s_tview[4][kTriViews];          // {view, dx, dy} of each neighbour slot
     __shared__ int s_term[4][64];                     // the valid smoothness terms, in term order
+    __shared__ float s_di[4][8][9];                   // the candidate's plane at the 9 sample points
     const int w = threadIdx.x >> 6;
     // compacted smoothness terms: the far terms that leave the superpixel map
     // (most of them at S = 8 in the first iterations: 61 terms, ~8 valid) take
@@ -628,7 +627,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
           s_prod[w][t][j] = simi * expf_neg_sq(diff, c.alpha);
         }
       }
-      if (ok) view_tasks(p, pd, n0, n1, n2, r, L, nv, s_toff[w], s_tview[w], s_samp[w][t], s_sflg[w][t]);
+      // the candidate plane at the 9 sample points (plane_at_r, as comp_consistency)
+      for (int sm = r; sm < 9; sm += L)
+        if (ok) {
+          const int2 o = s_toff[w][sm];
+          s_di[w][t][sm] = plane_at_r(n0, n1, n2, rn2, p.cx, p.cy, pd, (float)((int)p.cx + o.x),
+                                      (float)((int)p.cy + o.y));
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ok) view_tasks(p, r, L, nv, s_toff[w], s_tview[w], s_di[w][t], s_samp[w][t], s_sflg[w][t]);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

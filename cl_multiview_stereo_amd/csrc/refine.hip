@@ -26,6 +26,13 @@ struct RArgs {
 
 __device__ __forceinline__ float expf_neg_sq(float diff, float k) { return mvs_expf(((-diff) * diff) * k); }
 
+// roundf(v) as truncf(v + copysignf(0.49999997f, v)): equal for every non-NaN
+// float (checked exhaustively over all 2^32 encodings, tests/test_oracle_cpu.py
+// test_round_half_away_identity); 3 VALU instead of ~6.  NaN stays NaN.
+__device__ __forceinline__ float round_ha(float v) {
+  return truncf(v + copysignf(__int_as_float(0x3effffff), v));
+}
+
 __device__ __forceinline__ float plane_at(float nx, float ny, float nz, float cx, float cy, float d, float px,
                                           float py) {
   float t = nx * (cx - px);
@@ -358,8 +365,8 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, int r, int L, int nv, 
         const int view = __float_as_int(tv.x);
         const float sxf = (float)(cxi + o.x), syf = (float)(cyi + o.y);
         di[i] = sdi[sm];  // the candidate plane at sample sm (view-independent, computed once)
-        xp[i] = (int)(sxf - roundf(di[i] * tv.y));
-        yp[i] = (int)(syf - roundf((c.bl * di[i]) * tv.z));
+        xp[i] = (int)(sxf - round_ha(di[i] * tv.y));
+        yp[i] = (int)(syf - round_ha((c.bl * di[i]) * tv.z));
         ok[i] = xp[i] >= 0 && yp[i] >= 0 && xp[i] < c.W && yp[i] < c.H;
         ip[i] = p.labels[P * view + (ok[i] ? (long)c.W * yp[i] + xp[i] : 0)];
         vw[i] = view;
@@ -814,7 +821,6 @@ __global__ __launch_bounds__(256) void k_spixl_to_image4(const float* __restrict
 }
 
 // ---- cross-view filter -------------------------------------------------------
-__device__ __forceinline__ float round_ha(float v);
 // Filter grid orders.  RM = false: (x tiles, rows, reference groups), so a
 // reference group streams the whole disparity stack before the next one
 // starts.  RM = true: (x tiles x reference groups, rows): every reference of
@@ -1270,12 +1276,6 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_lds(const float* __re
   out[P * r + p] = dest;
 }
 
-// roundf(v) as truncf(v + copysignf(0.49999997f, v)): equal for every non-NaN
-// float (checked exhaustively over all 2^32 encodings, tests/test_oracle_cpu.py
-// test_round_half_away_identity); 3 VALU instead of ~6.  NaN stays NaN.
-__device__ __forceinline__ float round_ha(float v) {
-  return truncf(v + copysignf(__int_as_float(0x3effffff), v));
-}
 
 // The same answer with one work queue per lane.  k_remove_incons_lds walks
 // candidates in lock-step: a wave runs every candidate until the LAST of its

@@ -41,25 +41,17 @@ __device__ __forceinline__ float plane_at(float nx, float ny, float nz, float cx
   return t / nz;
 }
 
-// t / b for a divisor b shared by many quotients, with y = 1.0f / b (IEEE):
-// q0 = t*y, one FMA remainder, one FMA correction -- the correctly rounded
-// quotient (Markstein; 4e8 random pairs incl. all-ones significands agree bit
-// for bit with IEEE division), 3 VALU ops instead of the ~47-cycle IEEE divide
-// sequence.  Zero, infinite, NaN and tiny/huge quotients take the IEEE divide.
-__device__ __forceinline__ float div_shared(float t, float b, float y) {
-  const float q0 = t * y;
-  const float r = __builtin_fmaf(-q0, b, t);
-  const float q1 = __builtin_fmaf(r, y, q0);
-  const float a = fabsf(q1);
-  return (a >= 1e-30f && a < 1e30f) ? q1 : t / b;
-}
-// plane_at with the divisor's reciprocal precomputed (bit-identical)
+// plane_at with the divisor's reciprocal at hand (callers compute 1/nz once).
+// The quotient is the IEEE division: a shared-reciprocal form (t*y, one FMA
+// remainder, one FMA correction, IEEE fallback outside [1e-30, 1e30)) is
+// bit-identical, but the compiler if-converts its fallback and evaluates the
+// whole divide sequence for every lane anyway -- measured 1 % slower than the
+// plain divide on the reference-defaults step (15.05 vs 14.90 ms), and 3 %
+// slower with the fallback forced into a real branch.
 __device__ __forceinline__ float plane_at_r(float nx, float ny, float nz, float rnz, float cx, float cy, float d,
                                             float px, float py) {
-  float t = nx * (cx - px);
-  t = t + ny * (cy - py);
-  t = t + nz * d;
-  return div_shared(t, nz, rnz);
+  (void)rnz;
+  return plane_at(nx, ny, nz, cx, cy, d, px, py);
 }
 
 __device__ __forceinline__ int step_size_of(float flx, float kss) {

@@ -57,55 +57,96 @@ __host__ __device__ __forceinline__ long pair_index(int y, int x, int W) {
 }
 
 // ---- window statistics + packed intensities ------------------------------
-// one workgroup = 64 columns x 16 rows of one view; the (16+2R) x (64+8)
-// byte tile is staged in LDS once.  The dummy row H of an odd-height image
-// is written as an invalid window.
+// one workgroup = 64 columns x 16 rows of one view; the (16+2R) x 76 byte
+// tile (image columns x0-4 .. x0+71) is staged in LDS once, by aligned 4-byte
+// loads when W % 4 == 0.  A thread owns one column and two row pairs: per
+// tile row it takes the 8 bytes starting at its window's left column (three
+// LDS dwords + v_alignbyte), whose first K give the horizontal sums
+// (v_sad_u8 against 0) and sums of squares (v_dot4_u32_u8 with itself); the
+// vertical sums slide over those rows.  Each row pair is written as one
+// 16-byte store per plane (rows 2m, 2m+1 are adjacent in the pair layout).
+// All sums are exact integers, so the planes are the ones the per-tap loop
+// made.  The dummy row H of an odd-height image is written as an invalid
+// window.
 constexpr int BS_TW = 64, BS_TH = 16;
 template <int R>
 __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q, int W, int H,
                                                    int z0, uint2* __restrict__ stats, uint2* __restrict__ pk) {
-  constexpr int K = 2 * R + 1, NK = K * K;
-  constexpr int TW = BS_TW + 8, TR = BS_TH + 2 * R;  // tile covers columns x0-R .. x0+63-R+7
-  __shared__ uint8_t t[TR][TW + 4];
+  constexpr int K = 2 * R + 1, NK = K * K, NR = 4 + 2 * R;
+  constexpr int TW = BS_TW + 12, TR = BS_TH + 2 * R, ND = TW / 4, OFF = 4 - R;
+  static_assert(R <= 3, "the window's K taps must fit the 8 bytes a thread takes per row");
+  __shared__ uint32_t t[TR][ND + 1];  // byte column c of a row = image column x0 - 4 + c
   const int x0 = blockIdx.x * BS_TW, y0 = blockIdx.y * BS_TH, z = z0 + blockIdx.z;
   const int Hp = H + (H & 1);
   const long Pv = (long)W * Hp;  // plane elements per view
   const uint8_t* Q = q + z * (long)W * H;
-  for (int i = threadIdx.x; i < TR * TW; i += 256) {
-    int r = i / TW, c = i % TW;
-    int yy = y0 - R + r, xx = x0 - R + c;
-    t[r][c] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? Q[(long)yy * W + xx] : 0;
+  if ((W & 3) == 0 && ((uintptr_t)q & 3) == 0) {  // rows start on 4-byte boundaries: a dword is wholly in or out
+    for (int i = threadIdx.x; i < TR * ND; i += 256) {
+      const int r = i / ND, d = i - r * ND;
+      const int yy = y0 - R + r, xx = x0 - 4 + 4 * d;
+      t[r][d] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? *(const uint32_t*)(Q + (long)yy * W + xx) : 0u;
+    }
+  } else {
+    for (int i = threadIdx.x; i < TR * ND; i += 256) {
+      const int r = i / ND, d = i - r * ND;
+      const int yy = y0 - R + r;
+      uint32_t v = 0;
+      if (yy >= 0 && yy < H) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int xx = x0 - 4 + 4 * d + b;
+          if (xx >= 0 && xx < W) v |= (uint32_t)Q[(long)yy * W + xx] << (8 * b);
+        }
+      }
+      t[r][d] = v;
+    }
   }
   __syncthreads();
-  const int lx = threadIdx.x & 63, ly0 = (threadIdx.x >> 6) * 4;  // 4 rows per thread
+  const int lx = threadIdx.x & 63, ly0 = (threadIdx.x >> 6) * 4;  // two row pairs per thread
   const int x = x0 + lx;
   if (x >= W) return;
+  const int c0 = lx + OFF, dw = c0 >> 2, sh = c0 & 3;  // image column x - R
+  constexpr uint32_t hmask = K == 7 ? 0x00ffffffu : K == 5 ? 0x000000ffu : 0u;
+  uint32_t lo[NR], hi[NR];
+  int hs[NR], hq[NR];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int ly = ly0 + k, y = y0 + ly;
-    if (y >= Hp) break;
-    int s = 0, ss = 0;
+  for (int r = 0; r < NR; r++) {
+    const uint32_t d0 = t[ly0 + r][dw], d1 = t[ly0 + r][dw + 1], d2 = t[ly0 + r][dw + 2];
+    lo[r] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    hi[r] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t hk = K == 3 ? 0u : hi[r] & hmask;
+    const uint32_t lk = K == 3 ? lo[r] & 0x00ffffffu : lo[r];
+    hs[r] = (int)__builtin_amdgcn_sad_u8(hk, 0u, __builtin_amdgcn_sad_u8(lk, 0u, 0u));
+    hq[r] = (int)__builtin_amdgcn_udot4(hk, hk, __builtin_amdgcn_udot4(lk, lk, 0u, false), false);
+  }
 #pragma unroll
-    for (int j = 0; j < K; j++)
+  for (int m = 0; m < 2; m++) {
+    const int y = y0 + ly0 + 2 * m;
+    if (y >= Hp) break;  // Hp and y are even: a pair is wholly in or out
+    float av[2], bv[2];
+    uint32_t w[4];
 #pragma unroll
-      for (int i = 0; i < K; i++) {
-        int v = t[ly + j][lx + i];
-        s += v;
-        ss += v * v;
+    for (int e = 0; e < 2; e++) {
+      const int k = 2 * m + e, yy = y + e;
+      int s = 0, ss = 0;
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        s += hs[k + j];
+        ss += hq[k + j];
       }
-    const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
-    const int var = NK * ss - s * s;
-    const float sv = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
-    const float av = (float)NK * sv;
-    const float bv = (float)(s - 128 * NK) * sv;  // centred window sum Sp' * s
-    float* st = (float*)stats + z * Pv * 2 + (((long)(y >> 1) * W + x) << 2) + (y & 1);
-    st[0] = av;
-    st[2] = bv;
-    const uint8_t* row = &t[ly + R][lx];
-    unsigned lo = row[0] | (row[1] << 8) | (row[2] << 16) | ((unsigned)row[3] << 24);
-    unsigned hi = row[4] | (row[5] << 8) | (row[6] << 16) | ((unsigned)row[7] << 24);
-    // q - 128 as int8 is q ^ 0x80
-    pk[z * Pv + pair_index(y, x, W)] = y < H ? make_uint2(lo ^ 0x80808080u, hi ^ 0x80808080u) : make_uint2(0u, 0u);
+      const bool valid = x - R >= 0 && x + R < W && yy - R >= 0 && yy + R < H;
+      const int var = NK * ss - s * s;
+      const float sv = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
+      av[e] = (float)NK * sv;
+      bv[e] = (float)(s - 128 * NK) * sv;  // centred window sum Sp' * s
+      // q - 128 as int8 is q ^ 0x80
+      const bool in = yy < H;
+      w[2 * e] = in ? lo[k + R] ^ 0x80808080u : 0u;
+      w[2 * e + 1] = in ? hi[k + R] ^ 0x80808080u : 0u;
+    }
+    const long pi = ((long)(y >> 1) * W + x) << 1;  // pair_index(y, x, W), y even
+    *(float4*)((float*)stats + z * Pv * 2 + 2 * pi) = make_float4(av[0], av[1], bv[0], bv[1]);
+    *(uint4*)(pk + z * Pv + pi) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 

@@ -261,3 +261,57 @@ def test_sweep_spixl_transposed_vertical(engine, monkeypatch, bl):
     s = sp.clone()
     engine.sweep_spixl(lab, s, rep, cam, S, 12, 16)
     same(s[12:16], out["2"][12:16], "view sub-range")
+
+
+def _box_planes_np(l8: np.ndarray, K: int):
+    """numpy restatement of the window planes (include/mvs.h layout): per
+    (view, row pair, column) the floats {a(y), a(y+1), b(y), b(y+1)} with
+    a = K^2 / sqrt(var), b = (S - 128 K^2) / sqrt(var) (NaN where the window
+    leaves the image, 0 where var == 0), and the 8 bytes from column x - R of
+    each row as int8 (q ^ 0x80; the dummy row H of an odd height and columns
+    outside the image as 0 ^ 0x80, the dummy row's 8 bytes as 0)."""
+    V, H, W = l8.shape
+    R, NK = K // 2, K * K
+    Hp = H + (H & 1)
+    pad = np.zeros((V, Hp + 2 * R, W + 8 + R), np.int64)
+    pad[:, R:R + H, R:R + W] = l8
+    s = np.zeros((V, Hp, W), np.int64)
+    ss = np.zeros((V, Hp, W), np.int64)
+    for j in range(K):
+        for i in range(K):
+            v = pad[:, j:j + Hp, i:i + W]
+            s += v
+            ss += v * v
+    var = (NK * ss - s * s).astype(np.int32)
+    y = np.arange(Hp)[None, :, None]
+    x = np.arange(W)[None, None, :]
+    valid = (x - R >= 0) & (x + R < W) & (y - R >= 0) & (y + R < H)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sv = np.where(var != 0, np.float32(1) / np.sqrt(var.astype(np.float32)), np.float32(0)).astype(np.float32)
+    sv = np.where(valid, sv, np.float32(np.nan)).astype(np.float32)
+    av = (np.float32(NK) * sv).astype(np.float32)
+    bv = ((s - 128 * NK).astype(np.float32) * sv).astype(np.float32)
+    st = np.empty((V, Hp // 2, W, 4), np.float32)
+    st[..., 0], st[..., 1], st[..., 2], st[..., 3] = av[:, 0::2], av[:, 1::2], bv[:, 0::2], bv[:, 1::2]
+    rows = np.stack([pad[:, R:R + Hp, k:k + W] for k in range(8)], -1).astype(np.uint8) ^ 0x80  # column x - R + k
+    rows[:, H:] = 0
+    pk = rows.reshape(V, Hp // 2, 2, W, 8).transpose(0, 1, 3, 2, 4).reshape(V, Hp // 2, W, 16)
+    return st, pk
+
+
+@pytest.mark.parametrize("K", [5, 7])
+@pytest.mark.parametrize("W,H", [(160, 37), (150, 40), (67, 21), (64, 16)])
+def test_box_planes(engine, K, W, H):
+    """k_box_stats against a numpy restatement, bit-exact: widths on and off
+    4-byte rows (the dword and byte tile fills), odd heights (the dummy row),
+    partial 64-column tiles."""
+    rng = np.random.default_rng(W * 1000 + H + K)
+    l8 = rng.integers(0, 256, (3, H, W), dtype=np.uint8)
+    l8[1, :, : W // 2] = 77  # flat windows: var == 0
+    box = engine.box_stats(torch.from_numpy(l8).cuda(), K).cpu().numpy()
+    Hp = H + (H & 1)
+    st, pk = _box_planes_np(l8, K)
+    got_st = box[0].reshape(-1).view(np.float32).reshape(3, Hp // 2, W, 4)
+    got_pk = box[1].reshape(-1).view(np.uint8).reshape(3, Hp // 2, W, 16)
+    same(got_st, st, f"stats K{K} {W}x{H}")
+    assert np.array_equal(got_pk, pk), f"packed rows K{K} {W}x{H}"

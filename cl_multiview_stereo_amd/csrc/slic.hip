@@ -542,31 +542,39 @@ __global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__
   }
 }
 
-__global__ void k_update_finalize(const float* __restrict__ part, int mw, int mh, int S, int G, int cpl, int ntx,
-                                  int nty, float* __restrict__ spixl) {
-  const int sp = blockIdx.x * blockDim.x + threadIdx.x, z = blockIdx.y;
-  if (sp >= mw * mh) return;
-  const int gx = sp % mw, gy = sp / mw, s16 = S / 16;
-  const float* pp = part + ((long)z * mw * mh + sp) * G * 6;
-  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+// 8 lanes per superpixel, lane c < 6 summing channel c of the G partials in
+// tile order (the reference's order; a tile outside the image adds an exact
+// +0, which leaves the running sum unchanged: it starts at +0 and a sum is
+// -0 only when both terms are).  All G loads are independent of the sums,
+// so they are issued ahead -- one thread walking all six channels was
+// load-latency-bound (14 us per launch at C2).
+__global__ __launch_bounds__(256) void k_update_finalize(const float* __restrict__ part, int mw, int mh, int S,
+                                                         int G, int cpl, int ntx, int nty,
+                                                         float* __restrict__ spixl) {
+  const int c = threadIdx.x & 7, sp = blockIdx.x * 32 + (threadIdx.x >> 3), z = blockIdx.y;
+  const bool live = sp < mw * mh;  // no early exit: lanes exchange the count below
+  const int spc = live ? sp : 0;
+  const int gx = spc % mw, gy = spc / mw, s16 = S / 16;
+  const float* pp = part + ((long)z * mw * mh + spc) * G * 6 + (c < 6 ? c : 5);
+  float acc = 0.f;
+  int tx = 0, ty = 0;
+#pragma unroll 4
   for (int t = 0; t < G; t++) {
-    const int TX = (gx - 1) * s16 + t % cpl, TY = (gy - 1) * s16 + t / cpl;
-    if (TX < 0 || TY < 0 || TX >= ntx || TY >= nty) continue;  // outside the image: the reference adds 0
-#pragma unroll
-    for (int ch = 0; ch < 6; ch++) acc[ch] = acc[ch] + pp[t * 6 + ch];
+    const int TX = (gx - 1) * s16 + tx, TY = (gy - 1) * s16 + ty;
+    const bool in = TX >= 0 && TY >= 0 && TX < ntx && TY < nty;  // outside the image: the reference adds 0
+    const float v = pp[t * 6];
+    acc = acc + (in ? v : 0.f);
+    if (++tx == cpl) { tx = 0; ty++; }
   }
+  const float n = __shfl(acc, (threadIdx.x & 63 & ~7) + 5);
+  if (!live || c > 6) return;
   float* o = spixl + 8 * ((long)z * mw * mh + sp);
-  const float n = acc[5];
-  o[0] = (float)sp;
-  if (n != 0) {
-    o[1] = acc[0] / n;
-    o[2] = acc[1] / n;
-    o[3] = acc[2] / n;
-    o[4] = acc[3] / n;
-    o[5] = acc[4] / n;
+  if (c == 6) {
+    o[0] = (float)sp;
+  } else if (c == 5) {
     o[6] = n;
   } else {
-    o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
+    o[1 + c] = n != 0 ? acc / n : 0.0f;
   }
 }
 
@@ -667,7 +675,7 @@ int launch_update_finalize(hipStream_t s, const float* part, int V, int W, int H
   int mw = map_dim(W, S), mh = map_dim(H, S);
   int G = (3 * S / kLocal) * (3 * S / kLocal), cpl = S * 3 / kLocal;
   int ntx = (W + 15) / 16, nty = (H + 15) / 16;
-  hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 63) / 64, V), dim3(64), 0, s, part, mw, mh, S, G, cpl, ntx,
+  hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 31) / 32, V), dim3(256), 0, s, part, mw, mh, S, G, cpl, ntx,
                      nty, spixl);
   MVS_LAUNCH_CHECK("k_update_finalize");
   return 0;
@@ -691,7 +699,7 @@ int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V
     hipLaunchKernelGGL(k_update_tiles, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, labels,
                        W, H, S, mw, mh, G, cpl, ntx, nty, part);
     MVS_LAUNCH_CHECK("k_update_tiles");
-    hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 63) / 64, V), dim3(64), 0, s, part, mw, mh, S, G, cpl,
+    hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 31) / 32, V), dim3(256), 0, s, part, mw, mh, S, G, cpl,
                        ntx, nty, spixl);
     MVS_LAUNCH_CHECK("k_update_finalize");
     return 0;

@@ -57,17 +57,29 @@ __device__ __forceinline__ float4 rgb2lab(uint32_t px) {
   return make_float4(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz), 0.0f);
 }
 
+// Each wave converts 256 consecutive pixels per pass, lane l taking pixels
+// l, l + 64, l + 128, l + 192: four independent conversions in flight per
+// thread, every load and store still wave-contiguous.
 __global__ __launch_bounds__(256) void k_cvt(const uint32_t* __restrict__ rgbx, long n, float4* __restrict__ lab,
                                              uint8_t* __restrict__ l8) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float4 v = rgb2lab(__builtin_nontemporal_load(rgbx + i));
-    lab[i] = v;
-    if (l8) {
-      // build-defined NCC intensity: clamp((int)(L*2.55f + 0.5f), 0, 255)
-      float t = v.x * 2.55f;
-      t = t + 0.5f;
-      int q = (int)t;
-      l8[i] = (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+  const long stride = (long)gridDim.x * 1024;
+  for (long c = ((long)blockIdx.x * 256 + (threadIdx.x & ~63)) * 4 + (threadIdx.x & 63); c < n; c += stride) {
+    uint32_t px[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) px[u] = c + 64 * u < n ? __builtin_nontemporal_load(rgbx + c + 64 * u) : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const long i = c + 64 * u;
+      if (i >= n) break;
+      const float4 v = rgb2lab(px[u]);
+      lab[i] = v;
+      if (l8) {
+        // build-defined NCC intensity: clamp((int)(L*2.55f + 0.5f), 0, 255)
+        float t = v.x * 2.55f;
+        t = t + 0.5f;
+        const int q = (int)t;
+        l8[i] = (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+      }
     }
   }
 }
@@ -605,8 +617,8 @@ __global__ void k_suppress(const uint32_t* __restrict__ in, uint32_t* __restrict
 
 int launch_cvt(hipStream_t s, const uint8_t* rgbx, long npix, float* lab, uint8_t* l8) {
   if (npix <= 0) return 0;
-  long blocks = (npix + 255) / 256;
-  if (blocks > 256L * 64) blocks = 256L * 64;
+  long blocks = (npix + 1023) / 1024;  // 1024 pixels per 256-thread block and pass
+  if (blocks > 256L * 32) blocks = 256L * 32;
   hipLaunchKernelGGL(k_cvt, dim3((unsigned)blocks), dim3(256), 0, s, (const uint32_t*)rgbx, npix, (float4*)lab, l8);
   MVS_LAUNCH_CHECK("k_cvt");
   return 0;

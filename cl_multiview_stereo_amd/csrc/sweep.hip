@@ -31,38 +31,55 @@ namespace mvs {
 namespace {
 
 // ---- find_super_pixel_boundary, clcode.cl:791-855 -------------------------
-__global__ void k_boundary(const float* __restrict__ spixl, const uint32_t* __restrict__ labels, int W, int H,
-                           int S, int mw, int mh, uint8_t* __restrict__ rep) {
-  int tx = blockIdx.x * blockDim.x + threadIdx.x, ty = blockIdx.y, z = blockIdx.z;
-  if (tx >= mw) return;
-  long M = (long)mw * mh, P = (long)W * H;
-  long s = (long)ty * mw + tx;
+// One wave per superpixel.  The reference walks i = 1 .. S-1 along 8
+// directions from the (clamped) centre and keeps, per direction, i - 1 of the
+// last i whose pixel still carries the superpixel's label: a maximum over
+// independent tests.  Lane 8k + j tests direction k at i = 1 + j + 8m, so the
+// 8 (S - 1) label gathers issue together instead of as one thread's chain
+// (C2: 30 -> see DESIGN.md), and an xor-butterfly takes each direction's
+// maximum.  Integer results: identical.
+__global__ __launch_bounds__(256) void k_boundary(const float* __restrict__ spixl,
+                                                  const uint32_t* __restrict__ labels, int W, int H, int S, int mw,
+                                                  int mh, uint8_t* __restrict__ rep) {
+  const int lane = threadIdx.x & 63;
+  const long s = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int z = blockIdx.y;
+  const long M = (long)mw * mh, P = (long)W * H;
+  if (s >= M) return;  // whole wave
   const float* sp = spixl + 8 * (z * M + s);
   int cx = (int)sp[1], cy = (int)sp[2];
   if (cx < S) cx += (S - cx);
   if (cx + S > W) cx -= S;
   if (cy < S) cy += (S - cy);
   if (cy + S > H) cy -= S;
-  uint32_t id = (uint32_t)(ty * mw + tx);
+  const uint32_t id = (uint32_t)s;
   const uint32_t* L = labels + z * P;
-  auto lbl = [&](int yy, int xx) -> uint32_t {
-    return (yy >= 0 && yy < H && xx >= 0 && xx < W) ? L[(long)yy * W + xx] : 0xFFFFFFFFu;
-  };
-  uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0, d6 = 0, d7 = 0;
-  for (int i = 1; i < S; i++) {
-    if (id == lbl(cy - i, cx - i) && cx - i >= 0 && cy - i >= 0) d0 = i - 1;
-    if (id == lbl(cy, cx - i) && cx - i >= 0) d1 = i - 1;
-    if (id == lbl(cy + i, cx - i) && cx - i >= 0 && cy + i < H) d2 = i - 1;
-    if (id == lbl(cy - i, cx) && cy - i >= 0) d3 = i - 1;
-    if (id == lbl(cy + i, cx) && cy + i < H) d4 = i - 1;
-    if (id == lbl(cy - i, cx + i) && cx + i < W && cy - i >= 0) d5 = i - 1;
-    if (id == lbl(cy, cx + i) && cx + i < W) d6 = i - 1;
-    if (id == lbl(cy + i, cx + i) && cx + i < W && cy + i < H) d7 = i - 1;
+  const int k = lane >> 3, j = lane & 7;
+  // direction k: (dx, dy) in the reference's order d0 .. d7
+  const int dx = k < 3 ? -1 : (k < 5 ? 0 : 1);
+  const int dy = (k == 0 || k == 3 || k == 5) ? -1 : ((k == 1 || k == 6) ? 0 : 1);
+  int d = 0;
+  for (int i0 = 1; i0 < S; i0 += 32) {
+    uint32_t v[4];
+    bool in[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {  // unconditional (clamped) loads: all four in flight together
+      const int i = i0 + j + 8 * m, xx = cx + dx * i, yy = cy + dy * i;
+      in[m] = i < S && xx >= 0 && xx < W && yy >= 0 && yy < H;
+      v[m] = L[in[m] ? (long)yy * W + xx : 0];
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+      if (in[m] && v[m] == id) d = i0 + j + 8 * m - 1;  // i grows: the last hit is the largest
   }
-  uint2 packed;
-  packed.x = (d0 & 0xff) | ((d1 & 0xff) << 8) | ((d2 & 0xff) << 16) | ((d3 & 0xff) << 24);
-  packed.y = (d4 & 0xff) | ((d5 & 0xff) << 8) | ((d6 & 0xff) << 16) | ((d7 & 0xff) << 24);
-  *(uint2*)(rep + 8 * (z * M + s)) = packed;
+  d = max(d, __shfl_xor(d, 1));
+  d = max(d, __shfl_xor(d, 2));
+  d = max(d, __shfl_xor(d, 4));
+  uint32_t w = (uint32_t)(d & 0xff) << (8 * (k & 3));
+  w |= __shfl_xor(w, 8);
+  w |= __shfl_xor(w, 16);  // lane 0: directions 0-3, lane 32: directions 4-7
+  const uint32_t hi = __shfl(w, 32);
+  if (lane == 0) *(uint2*)(rep + 8 * (z * M + s)) = make_uint2(w, hi);
 }
 
 // ---- initial_depth_estimation_v2, clcode.cl:972-1069 ----------------------
@@ -89,7 +106,10 @@ struct SweepArgs {
 // 2 (dx == dy: sheared, at (x - y + H - 1) H + y) or 3 (dx == -dy: at
 // (x + y) H + y).  With bl != 1 the diagonal shifts drift apart by a row
 // every 1/|bl - 1| levels: still a few lines per instruction instead of 64.
-template <int LPS>
+// TL = false (no re-laid views in this call, e.g. a horizontal array): the
+// row-major addressing folds to yp W + xp at compile time -- the general
+// form's extra multiply-add per tap cost C2 (5x1 array) 173 -> 224 us.
+template <int LPS, bool TL>
 __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ lab, float* __restrict__ spixl,
                                                      const uint8_t* __restrict__ rep,
                                                      const float* __restrict__ levels, const int* __restrict__ vs,
@@ -145,13 +165,13 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       float fdx = d * (float)(vx - rx);
       float fdy = (a.bl * d) * (float)(vy - ry);
       const int ddx = vx - rx, ddy = vy - ry;
-      const int kind = !labT ? 0 : ddx == 0 ? 1 : ddx == ddy ? 2 : ddx == -ddy ? 3 : 0;
-      const int ts = kind ? tslot[4 * view + kind] : -1;
-      const float4* labv = ts >= 0 ? labT + (long)ts * tstride : lab + (long)view * P;
+      const int kind = !TL ? 0 : ddx == 0 ? 1 : ddx == ddy ? 2 : ddx == -ddy ? 3 : 0;
+      const int ts = TL && kind ? tslot[4 * view + kind] : -1;
+      const float4* labv = TL && ts >= 0 ? labT + (long)ts * tstride : lab + (long)view * P;
       // element index = off + x sxs + y sys in the view's layout
-      const int sxs = ts < 0 ? 1 : a.H;
-      const int sys = ts < 0 ? a.W : kind == 1 ? 1 : kind == 2 ? 1 - a.H : a.H + 1;
-      const int off = ts >= 0 && kind == 2 ? (a.H - 1) * a.H : 0;
+      const int sxs = !TL || ts < 0 ? 1 : a.H;
+      const int sys = !TL || ts < 0 ? a.W : kind == 1 ? 1 : kind == 2 ? 1 - a.H : a.H + 1;
+      const int off = TL && ts >= 0 && kind == 2 ? (a.H - 1) * a.H : 0;
       float val = 0.0f;
       // branch-free taps: every load is issued (out-of-image taps read pixel 0
       // and are dropped by the select), so the 25 gathers of a neighbour are
@@ -686,7 +706,7 @@ __global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vol, cons
 int launch_boundary(hipStream_t s, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
                     uint8_t* rep) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
-  hipLaunchKernelGGL(k_boundary, dim3((mw + 63) / 64, mh, V), dim3(64), 0, s, spixl, labels, W, H, S, mw, mh, rep);
+  hipLaunchKernelGGL(k_boundary, dim3((mw * mh + 3) / 4, V), dim3(256), 0, s, spixl, labels, W, H, S, mw, mh, rep);
   MVS_LAUNCH_CHECK("k_boundary");
   return 0;
 }
@@ -779,9 +799,10 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
       labT = buf;
     }
   }
-  hipLaunchKernelGGL(half ? k_sweep_spixl<32> : k_sweep_spixl<64>, dim3((unsigned)(8 * ((nb + 7) / 8)),
-                     (unsigned)(z1 - z0)), dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a, wps,
-                     labT, tslot, tstride);
+  auto kern = labT ? (half ? k_sweep_spixl<32, true> : k_sweep_spixl<64, true>)
+                   : (half ? k_sweep_spixl<32, false> : k_sweep_spixl<64, false>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(8 * ((nb + 7) / 8)), (unsigned)(z1 - z0)), dim3(256), 0, s,
+                     (const float4*)lab, spixl, rep, levels, vs, sn, a, wps, labT, tslot, tstride);
   MVS_LAUNCH_CHECK("k_sweep_spixl");
   return 0;
 }

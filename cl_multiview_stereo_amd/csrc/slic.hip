@@ -104,6 +104,7 @@ __global__ void k_init_centers(const float4* __restrict__ lab, int W, int H, int
   o[4] = c.y;
   o[5] = c.z;
   o[6] = 0.0f;
+  o[7] = 0.0f;  // s7 (disparity) is never written by the reference's SLIC: its buffer starts at 0
 }
 
 // ---- edge_compute_alternative, clcode.cl:161-195 -------------------------

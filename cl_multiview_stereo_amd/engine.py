@@ -139,8 +139,9 @@ class Engine:
         intended centre perturbation."""
         V, H, W, _ = lab.shape
         mw, mh = map_size(W, H, S)
-        # s7 (disparity) is never written by SLIC (clcode.cl:285-293): start from zeros
-        spixl = torch.zeros((V, mh, mw, 8), dtype=torch.float32, device=self.device) if spixl is None else spixl
+        # s7 (disparity) is never written by the reference's SLIC (clcode.cl:285-293);
+        # k_init_centers zeroes it, so every word of spixl is written
+        spixl = self.empty((V, mh, mw, 8), torch.float32) if spixl is None else spixl
         labels = self.empty((V, H, W), torch.int32) if labels is None else labels
         if spixl.shape != (V, mh, mw, 8) or labels.shape != (V, H, W):
             raise ValueError("slic: output shapes do not match")
@@ -153,7 +154,7 @@ class Engine:
     def grid(self, lab: torch.Tensor, S: int):
         V, H, W, _ = lab.shape
         mw, mh = map_size(W, H, S)
-        spixl = torch.zeros((V, mh, mw, 8), dtype=torch.float32, device=self.device)
+        spixl = self.empty((V, mh, mw, 8), torch.float32)  # every word written (s7 = 0)
         labels = self.empty((V, H, W), torch.int32)
         self._stream()
         _lib.check(self.L.mvs_grid_d(self.ctx, _ptr(lab), V, W, H, S, _ptr(spixl), _ptr(labels)), "mvs_grid_d")

@@ -103,7 +103,9 @@ int mvs_cvt_d(mvs_ctx* ctx, const uint8_t* rgbx, int V, int W, int H, float* lab
 /* SLIC on V views of lab (clSLIC::do_super_pixel_seg, clSLIC.cpp:67-122,
  * minus the cvt it starts with).  spixl [V][mh][mw][8], labels [V][H][W].
  * lab is read only, except with p->edge_enable == 1, where the reference's
- * edge step overwrites it (as clSLIC's lab_img_dev). */
+ * edge step overwrites it (as clSLIC's lab_img_dev).  Every spixl word is
+ * written; s7 (disparity, untouched by the reference's SLIC on its zeroed
+ * buffer) is set to 0. */
 int mvs_slic_d(mvs_ctx* ctx, float* lab, int V, int W, int H, const mvs_slic_params* p,
                float* spixl, uint32_t* labels);
 

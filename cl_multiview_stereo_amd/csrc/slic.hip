@@ -319,6 +319,10 @@ __device__ __forceinline__ float wave_tree(float v0, float v1, float v2, float v
 // reference's order (wave_tree), and lane 0 sums the tile partials in tile
 // order -- no LDS, no barriers, and no idle waves when G < 4 (S = 8: G = 3,
 // the third tile entirely outside the 3S window).
+// UT = tiles per chunk (below): 4 when the window has many tiles (C5, S = 40:
+// G = 57, update 39.1 -> 38.1 ms per C5 step), 1 for a few (S = 8: G = 3,
+// where the chunk's registers cost more occupancy than the latencies it hides).
+template <int UT>
 __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, const uint32_t* __restrict__ labels,
                                                 int W, int H, int S, int mw, int mh, int G, int cpl,
                                                 float* __restrict__ spixl) {
@@ -331,35 +335,60 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
   const uint32_t* I = labels + (long)z * P;
   const int lx = lane & 15, ly0 = lane >> 4;
   float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < G; t++) {
-    const int nbx = t % cpl, nby = t / cpl;
-    float v[4][6];
-    bool any = false;
+  // tiles in chunks of UT: every label of the chunk is gathered before any
+  // test, then every member's colour, so a chunk costs two memory latencies
+  // instead of two per tile; the trees and the partial sums keep tile order
+  for (int t0 = 0; t0 < G; t0 += UT) {
+    uint32_t lb[UT][4];
+    int pix[UT][4], bx[UT], by[UT];
 #pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const int ly = ly0 + 4 * m;
-      const int pxo = nbx * kLocal + lx, pyo = nby * kLocal + ly;
-      const int px = gx * S - S + pxo, py = gy * S - S + pyo;
-      const bool in = pyo < S * 3 && pxo < S * 3 && py >= 0 && px >= 0 && px < W && py < H;
-      bool mem = false;
-      if (in) mem = I[(long)py * W + px] == (uint32_t)sp;
-      float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (mem) c = L[(long)py * W + px];
-      v[m][0] = mem ? (float)px : 0.0f;
-      v[m][1] = mem ? (float)py : 0.0f;
-      v[m][2] = c.x;
-      v[m][3] = c.y;
-      v[m][4] = c.z;
-      v[m][5] = mem ? 1.0f : 0.0f;
-      any |= mem;
+    for (int u = 0; u < UT; u++) {
+      const int t = t0 + u, nbx = t % cpl, nby = t / cpl;
+      bx[u] = gx * S - S + nbx * kLocal;
+      by[u] = gy * S - S + nby * kLocal;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const int pxo = nbx * kLocal + lx, pyo = nby * kLocal + ly0 + 4 * m;
+        const int px = bx[u] + lx, py = by[u] + ly0 + 4 * m;
+        const bool in = t < G && pyo < S * 3 && pxo < S * 3 && py >= 0 && px >= 0 && px < W && py < H;
+        pix[u][m] = in ? py * W + px : -1;
+        lb[u][m] = I[in ? py * W + px : 0];
+      }
     }
-    float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (__any(any)) {
+    float4 c[UT][4];
 #pragma unroll
-      for (int c = 0; c < 6; c++) r[c] = wave_tree(v[0][c], v[1][c], v[2][c], v[3][c]);
+    for (int u = 0; u < UT; u++)
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const bool mem = pix[u][m] >= 0 && lb[u][m] == (uint32_t)sp;
+        c[u][m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (mem) c[u][m] = L[pix[u][m]];
+      }
+#pragma unroll
+    for (int u = 0; u < UT; u++) {
+      if (t0 + u >= G) break;
+      float v[4][6];
+      bool any = false;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const bool mem = pix[u][m] >= 0 && lb[u][m] == (uint32_t)sp;
+        const int px = bx[u] + lx, py = by[u] + ly0 + 4 * m;
+        v[m][0] = mem ? (float)px : 0.0f;
+        v[m][1] = mem ? (float)py : 0.0f;
+        v[m][2] = c[u][m].x;
+        v[m][3] = c[u][m].y;
+        v[m][4] = c[u][m].z;
+        v[m][5] = mem ? 1.0f : 0.0f;
+        any |= mem;
+      }
+      float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (__any(any)) {
+#pragma unroll
+        for (int ch = 0; ch < 6; ch++) r[ch] = wave_tree(v[0][ch], v[1][ch], v[2][ch], v[3][ch]);
+      }
+#pragma unroll
+      for (int ch = 0; ch < 6; ch++) acc[ch] = acc[ch] + r[ch];  // lane 0 holds the tile partial
     }
-#pragma unroll
-    for (int c = 0; c < 6; c++) acc[c] = acc[c] + r[c];  // lane 0 holds the tile partial
   }
   if (lane == 0) {
     float* o = spixl + 8 * ((long)z * mw * mh + sp);
@@ -717,8 +746,8 @@ int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V
     MVS_LAUNCH_CHECK("k_update_finalize");
     return 0;
   }
-  hipLaunchKernelGGL(k_update, dim3((mw * mh + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, labels, W, H, S, mw,
-                     mh, G, cpl, spixl);
+  hipLaunchKernelGGL(G > 4 ? k_update<4> : k_update<1>, dim3((mw * mh + 3) / 4, V), dim3(256), 0, s,
+                     (const float4*)lab, labels, W, H, S, mw, mh, G, cpl, spixl);
   MVS_LAUNCH_CHECK("k_update");
   return 0;
 }

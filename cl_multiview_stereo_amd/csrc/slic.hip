@@ -314,6 +314,18 @@ __device__ __forceinline__ float wave_tree(float v0, float v1, float v2, float v
   return s;
 }
 
+// The same tree shape over uint32 (integer sums: any order gives the same value).
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+  uint32_t s = (v0 + v2) + (v1 + v3);
+  s = s + __builtin_amdgcn_permlane32_swap(s, s, false, false)[1];
+  s = s + __builtin_amdgcn_permlane16_swap(s, s, false, false)[1];
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x108, 0xf, 0xf, true);
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x104, 0xf, 0xf, true);
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x102, 0xf, 0xf, true);
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x101, 0xf, 0xf, true);
+  return s;
+}
+
 // One WAVE per superpixel (4 per workgroup): the wave walks the G window
 // tiles in order, each tile's 256 pixels as 4 per lane, tree-reduced in the
 // reference's order (wave_tree), and lane 0 sums the tile partials in tile
@@ -569,12 +581,21 @@ __global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__
       }
       float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (__any(any)) {
-        r[0] = wave_tree(mem[0] ? fx[0] : 0.f, mem[1] ? fx[1] : 0.f, mem[2] ? fx[2] : 0.f, mem[3] ? fx[3] : 0.f);
-        r[1] = wave_tree(mem[0] ? fy[0] : 0.f, mem[1] ? fy[1] : 0.f, mem[2] ? fy[2] : 0.f, mem[3] ? fy[3] : 0.f);
+        // x, y and count are integers whose float trees are exact (sums < 2^24), so
+        // they come from one integer tree of packed tile-local fields: sum of
+        // x - 16 TX (<= 3840, bits 0-11), of y - 16 TY (bits 12-23) and the count
+        // (bits 24-31; 256 wraps to 0, and a tree only runs with a member present)
+        uint32_t pk[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) pk[m] = mem[m] ? (uint32_t)lx | (uint32_t)(ly0 + 4 * m) << 12 | 1u << 24 : 0u;
+        const uint32_t q = wave_sum_u32(pk[0], pk[1], pk[2], pk[3]);
+        const int cnt = (q >> 24) ? (int)(q >> 24) : 256;
+        r[0] = (float)((int)(q & 0xfffu) + cnt * 16 * TX);
+        r[1] = (float)((int)((q >> 12) & 0xfffu) + cnt * 16 * TY);
         r[2] = wave_tree(mem[0] ? c[0].x : 0.f, mem[1] ? c[1].x : 0.f, mem[2] ? c[2].x : 0.f, mem[3] ? c[3].x : 0.f);
         r[3] = wave_tree(mem[0] ? c[0].y : 0.f, mem[1] ? c[1].y : 0.f, mem[2] ? c[2].y : 0.f, mem[3] ? c[3].y : 0.f);
         r[4] = wave_tree(mem[0] ? c[0].z : 0.f, mem[1] ? c[1].z : 0.f, mem[2] ? c[2].z : 0.f, mem[3] ? c[3].z : 0.f);
-        r[5] = wave_tree(mem[0] ? 1.f : 0.f, mem[1] ? 1.f : 0.f, mem[2] ? 1.f : 0.f, mem[3] ? 1.f : 0.f);
+        r[5] = (float)cnt;
       }
       if (lane == 0) {
 #pragma unroll

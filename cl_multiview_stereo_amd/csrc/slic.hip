@@ -379,24 +379,28 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
 #pragma unroll
     for (int u = 0; u < UT; u++) {
       if (t0 + u >= G) break;
-      float v[4][6];
+      float v[4][3];
+      uint32_t pk[4];
       bool any = false;
 #pragma unroll
       for (int m = 0; m < 4; m++) {
         const bool mem = pix[u][m] >= 0 && lb[u][m] == (uint32_t)sp;
-        const int px = bx[u] + lx, py = by[u] + ly0 + 4 * m;
-        v[m][0] = mem ? (float)px : 0.0f;
-        v[m][1] = mem ? (float)py : 0.0f;
-        v[m][2] = c[u][m].x;
-        v[m][3] = c[u][m].y;
-        v[m][4] = c[u][m].z;
-        v[m][5] = mem ? 1.0f : 0.0f;
+        // x, y, count: one packed integer tree of tile-local fields (as k_assign_tiles)
+        pk[m] = mem ? (uint32_t)lx | (uint32_t)(ly0 + 4 * m) << 12 | 1u << 24 : 0u;
+        v[m][0] = c[u][m].x;
+        v[m][1] = c[u][m].y;
+        v[m][2] = c[u][m].z;
         any |= mem;
       }
       float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (__any(any)) {
+        const uint32_t q = wave_sum_u32(pk[0], pk[1], pk[2], pk[3]);
+        const int cnt = (q >> 24) ? (int)(q >> 24) : 256;
+        r[0] = (float)((int)(q & 0xfffu) + cnt * bx[u]);  // = the sum of member x: exact below 2^24
+        r[1] = (float)((int)((q >> 12) & 0xfffu) + cnt * by[u]);
 #pragma unroll
-        for (int ch = 0; ch < 6; ch++) r[ch] = wave_tree(v[0][ch], v[1][ch], v[2][ch], v[3][ch]);
+        for (int ch = 0; ch < 3; ch++) r[2 + ch] = wave_tree(v[0][ch], v[1][ch], v[2][ch], v[3][ch]);
+        r[5] = (float)cnt;
       }
 #pragma unroll
       for (int ch = 0; ch < 6; ch++) acc[ch] = acc[ch] + r[ch];  // lane 0 holds the tile partial

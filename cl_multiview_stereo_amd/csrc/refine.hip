@@ -142,22 +142,36 @@ __device__ float init_consistency(const RArgs& c, const float* __restrict__ spix
     int view = vs[z * c.V + n];
     int vx = view % c.aw, vy = view / c.aw;
     float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
-    for (int i = -1; i <= 1; i++)
-      for (int j = -1; j <= 1; j++) {
-        int xr = (int)cxf + smp[(i + 1) * 3 + j + 1] * i;
-        int yr = (int)cyf + smp[(i + 1) * 3 + j + 1] * j;
-        int xp = (int)((float)xr - roundf(d * (float)(vx - camx)));
-        int yp = (int)((float)yr - roundf((c.bl * d) * (float)(vy - camy)));
-        if (xp >= 0 && yp >= 0 && xp < c.W && yp < c.H) {
-          uint32_t ip = labels[P * view + (long)c.W * yp + xp];
-          uint32_t sx = ip % (uint32_t)c.mw, sy = ip / (uint32_t)c.mw;
-          const float* s = spixl + 8 * (M * view + (long)c.mw * sy + sx);
-          float diff = s[7] - d;
+    // the view's 9 label gathers, then the 9 records they name, are issued
+    // before the ordered sums (two memory latencies per view instead of 18);
+    // record (ip % mw, ip / mw) is record ip
+    bool okv[9];
+    uint32_t ipv[9];
+#pragma unroll
+    for (int t = 0; t < 9; t++) {
+      const int i = t / 3 - 1, j = t % 3 - 1;
+      const int xr = (int)cxf + smp[t] * i;
+      const int yr = (int)cyf + smp[t] * j;
+      const int xp = (int)((float)xr - roundf(d * (float)(vx - camx)));
+      const int yp = (int)((float)yr - roundf((c.bl * d) * (float)(vy - camy)));
+      okv[t] = xp >= 0 && yp >= 0 && xp < c.W && yp < c.H;
+      ipv[t] = labels[P * view + (okv[t] ? (long)c.W * yp + xp : 0)];
+    }
+    float r3[9], r4[9], r5[9], r7[9];
+#pragma unroll
+    for (int t = 0; t < 9; t++) {
+      const float* s = spixl + 8 * (M * view + (okv[t] ? (long)ipv[t] : 0));
+      r3[t] = s[3]; r4[t] = s[4]; r5[t] = s[5]; r7[t] = s[7];
+    }
+#pragma unroll
+    for (int t = 0; t < 9; t++) {
+        if (okv[t]) {
+          float diff = r7[t] - d;
           float wv = fabsf(diff) < c.fuse ? 1.0f : 0.0f;
           visible = visible + wv * expf_neg_sq(diff, c.alpha);
           vis_w = vis_w + wv;
           occ_w = occ_w + (1.0f - wv);
-          diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+          diff = mvs_distance3(r3[t], r4[t], r5[t], color[0], color[1], color[2]);
           visibility = visibility + expf_neg_sq(diff, c.gamma);
           num = num + 1.0f;
         }

@@ -232,9 +232,10 @@ def _pmc_traffic(name, W, H, D):
 
 
 def _valu_insts(name, cost, fused, W, H, D):
-    """SQ_INSTS_VALU per launch of the NCC sweep from this configuration's own
-    PMC pass (profiles/pmc_ncc_<config>.json, scripts/profile.sh), launch-
-    weighted over the band-width variants; None without a pass of this shape."""
+    """SQ_INSTS_VALU per launch of the (plain, one view per launch) NCC sweep
+    from this configuration's own PMC pass (profiles/pmc_ncc_<config>.json,
+    scripts/profile.sh), launch-weighted over the band-width variants; None
+    without a pass of this shape."""
     pmc_ncc = os.path.join(ROOT, "profiles", f"pmc_ncc_{name}.json")
     if cost != "ncc" or not os.path.exists(pmc_ncc):
         return None
@@ -247,6 +248,20 @@ def _valu_insts(name, cost, fused, W, H, D):
         return None
     wts = [e.get("launches", 1) for e in ent]
     return sum(e["valu_wave_insts_per_launch"] * w for e, w in zip(ent, wts)) / sum(wts)
+
+
+def _valu_insts_fused_per_view(name, W, H, D):
+    """SQ_INSTS_VALU of the fused sweep per reference view: the PMC pass's
+    total over every FUSE=true launch divided by the reference views its bench
+    process swept (profile_counts.ncc_wta_views of that run's own JSON line,
+    recorded by scripts/summarize_prof.py as fused_valu_wave_insts_per_view)."""
+    p = os.path.join(ROOT, "profiles", f"pmc_ncc_{name}.json")
+    if not os.path.exists(p):
+        return None
+    j = json.load(open(p))
+    if (j.get("W"), j.get("H"), j.get("D")) != (W, H, D) or "fused_valu_wave_insts_per_view" not in j:
+        return None
+    return {"insts": j["fused_valu_wave_insts_per_view"], "source": j.get("source")}
 
 
 def bench(args, world, rank, local):
@@ -276,27 +291,37 @@ def bench(args, world, rank, local):
     vlists = params.nearest_neighbours(cfg["aw"], cfg["ah"], cfg["knn"]) if cfg.get("knn") else None
 
     # HIP events around the sweep / WTA launches, on the stream they run on
+    # (engine calls are enqueued on torch's current stream: Engine._stream).
+    # Every call is counted, timed or not, so a PMC pass of this same command
+    # can divide its counter totals by calls (scripts/summarize_prof.py).
     timers = {"wta": [], "ncc": [], "fused": []}
+    calls = {"wta": 0, "ncc": 0, "fused": 0, "fused_views": 0}
     recording = [False]
 
-    def instrument(name, fn):
+    def instrument(name, fn, views=None):
         def w(*a, **k):
             s = torch.cuda.Event(enable_timing=True)
             t = torch.cuda.Event(enable_timing=True)
             s.record()
             r = fn(*a, **k)
             t.record()
+            n = views(*a, **k) if views else 1
+            calls[name] += 1
+            if name == "fused":
+                calls["fused_views"] += n
             if recording[0]:
-                timers[name].append((s, t))
+                timers[name].append((s, t, n))
             return r
         return w
 
     e.wta = instrument("wta", e.wta)
     e.ncc_volume = instrument("ncc", e.ncc_volume)
     e.ncc_wta = instrument("fused", e.ncc_wta)
+    # the fused path of Pipeline: one call per run of reference views [z0, z1)
+    e.ncc_wta_range = instrument("fused", e.ncc_wta_range, views=lambda l8, box, cam, z0, z1, *a, **k: z1 - z0)
 
     def avg(lst):
-        return sum(s.elapsed_time(t) for s, t in lst) / len(lst) * 1e-3
+        return sum(s.elapsed_time(t) for s, t, _ in lst) / len(lst) * 1e-3
 
     def make(fz):
         p = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,
@@ -344,18 +369,25 @@ def bench(args, world, rank, local):
                    "refinement": bool(cfg.get("refine")), "consistency_filter": bool(cfg.get("filt"))},
     }
     if fused and head_timers["fused"]:
-        t_f = avg(head_timers["fused"])
+        t_f = avg(head_timers["fused"])  # per call (one run of reference views)
+        vpc = sum(n for _, _, n in head_timers["fused"]) / len(head_timers["fused"])
         cells = float(D) * W * H
         nbr = max(1, int(pipe.cam.subset_num[0]))
-        insts = _valu_insts(args.config, cost, True, W, H, D)
+        per_view = _valu_insts_fused_per_view(args.config, W, H, D)
         res["roofline_sweep"] = {
-            "kernel": "k_ncc_volume<..., FUSE=true> (sweep + WTA, the headline step's dominant kernel)",
-            "bound": "valu", "avg_launch_ms": round(t_f * 1e3, 4),
-            "view_cells_per_s": round(cells * nbr / t_f / 1e9, 3), "unit_view_cells": "G view-cells/s"}
-        if insts is not None:
-            res["roofline_sweep"].update({"valu_wave_insts_per_launch": round(insts),
-                                          "valu_issue_frac": round(insts / t_f / VALU_PEAK, 4),
-                                          "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op"})
+            "kernel": "k_ncc_volume<..., FUSE=true> (fused sweep + WTA, the headline step's dominant kernel)",
+            "bound": "valu", "avg_call_ms": round(t_f * 1e3, 4), "views_per_call": vpc,
+            "avg_ms_per_view": round(t_f * 1e3 / vpc, 4),
+            "view_cells_per_s": round(cells * nbr * vpc / t_f / 1e9, 3), "unit_view_cells": "G view-cells/s",
+            "timing": "HIP events around each mvs_ncc_wta_range_d call of the timed steps, on its stream"}
+        if per_view is not None:
+            res["roofline_sweep"].update({
+                "valu_wave_insts_per_view": round(per_view["insts"]),
+                "valu_issue_frac": round(per_view["insts"] * vpc / t_f / VALU_PEAK, 4),
+                "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op",
+                "valu_source": per_view["source"]})
+    res["profile_counts"] = {"ncc_wta_calls": calls["fused"], "ncc_wta_views": calls["fused_views"],
+                             "ncc_volume_calls": calls["ncc"], "wta_calls": calls["wta"]}
 
     # the two-pass step (cost volume in HBM + k_wta), same protocol: the
     # north star's roofline is k_wta's read of that volume

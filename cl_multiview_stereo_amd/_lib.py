@@ -29,8 +29,14 @@ class MvsError(RuntimeError):
 
 
 class SlicParams(C.Structure):
-    _fields_ = [("spixl_size", C.c_int), ("color_weight", C.c_float), ("no_iter", C.c_int),
-                ("enforce_connectivity", C.c_int), ("edge_enable", C.c_int)]
+    """mvs_slic_params (ABI 0.3): struct_size is filled in by the constructor."""
+    _fields_ = [("struct_size", C.c_uint32), ("spixl_size", C.c_int), ("color_weight", C.c_float),
+                ("no_iter", C.c_int), ("enforce_connectivity", C.c_int), ("edge_enable", C.c_int),
+                ("search", C.c_int)]
+
+    def __init__(self, spixl_size=8, color_weight=0.6, no_iter=5, enforce_connectivity=0, edge_enable=0, search=0):
+        super().__init__(C.sizeof(SlicParams), spixl_size, color_weight, no_iter, enforce_connectivity,
+                         edge_enable, search)
 
 
 class ArrayDesc(C.Structure):
@@ -40,8 +46,15 @@ class ArrayDesc(C.Structure):
 
 
 class RefineParams(C.Structure):
-    _fields_ = [("gamma", C.c_float), ("alpha", C.c_float), ("fuse", C.c_float), ("kernel_step", C.c_int),
-                ("kernel_size", C.c_int), ("no_prop", C.c_int), ("fusion_compat", C.c_int)]
+    """mvs_refine_params (ABI 0.3): struct_size is filled in by the constructor."""
+    _fields_ = [("struct_size", C.c_uint32), ("gamma", C.c_float), ("alpha", C.c_float), ("fuse", C.c_float),
+                ("kernel_step", C.c_int), ("kernel_size", C.c_int), ("no_prop", C.c_int),
+                ("fusion_compat", C.c_int), ("prescaled", C.c_int)]
+
+    def __init__(self, gamma=2.0, alpha=6.0, fuse=1.0, kernel_step=13, kernel_size=1080, no_prop=5,
+                 fusion_compat=1, prescaled=0):
+        super().__init__(C.sizeof(RefineParams), gamma, alpha, fuse, kernel_step, kernel_size, no_prop,
+                         fusion_compat, prescaled)
 
 
 _lib = None

@@ -153,7 +153,7 @@ void* scratch(mvs_ctx* ctx, size_t bytes, int* rc) {
 extern "C" {
 
 const char* mvs_last_error(void) { return g_err.c_str(); }
-const char* mvs_version(void) { return "mvs-mi355x 0.1 (gfx950)"; }
+const char* mvs_version(void) { return "mvs-mi355x 0.3 (gfx950)"; }
 
 int mvs_create(int device, mvs_ctx** out) {
   if (!out) return mvs::arg_fail("mvs_create: out is null");
@@ -209,10 +209,13 @@ int mvs_slic_d(mvs_ctx* c, float* lab, int V, int W, int H, const mvs_slic_param
                uint32_t* labels) {
   if (!c || !lab || !spixl || !labels || !p || V <= 0 || bad_dims(W, H))
     return mvs::arg_fail("mvs_slic_d: bad arguments");
+  if (p->struct_size != sizeof(mvs_slic_params))
+    return mvs::arg_fail("mvs_slic_d: struct_size != sizeof(mvs_slic_params) (caller built against another mvs.h)");
   int S = p->spixl_size;
   if (S < 6 || S > 96) return mvs::arg_fail("mvs_slic_d: spixl_size must be in [6, 96] (3S/16 > 0)");
   if (p->no_iter < 0) return mvs::arg_fail("mvs_slic_d: no_iter < 0");
   if (p->edge_enable < 0 || p->edge_enable > 2) return mvs::arg_fail("mvs_slic_d: edge_enable must be 0, 1 or 2");
+  if (p->search != 0 && p->search != 1) return mvs::arg_fail("mvs_slic_d: search must be 0 or 1");
   // clSLIC ctor, clSLIC.cpp:15-18 (host float arithmetic)
   float xy = 1.0f / (1.4242f * (float)S);
   float col = 15.0f / (1.7321f * 128.0f);
@@ -233,18 +236,18 @@ int mvs_slic_d(mvs_ctx* c, float* lab, int V, int W, int H, const mvs_slic_param
   if (part && S % 16 == 0) {
     // assign -> (update -> assign) x no_iter with each update's tile partials
     // produced by the assign pass before it (one Lab read per iteration)
-    RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels,
+    RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels,
                                 p->no_iter > 0 ? part : nullptr));
     for (int i = 0; i < p->no_iter; i++) {
       RC(mvs::launch_update_finalize(s, part, V, W, H, S, spixl));
-      RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels,
+      RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels,
                                   i + 1 < p->no_iter ? part : nullptr));
     }
   } else {
-    RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
+    RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels));
     for (int i = 0; i < p->no_iter; i++) {
       RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl, part));
-      RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, labels));
+      RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels));
     }
   }
   if (p->enforce_connectivity) {
@@ -395,13 +398,17 @@ int mvs_refine_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint
                  const mvs_array* a, const mvs_refine_params* p, float* flat, float* state, float* state2,
                  float* disp) {
   if (!c || !p || !flat || !state || !state2) return mvs::arg_fail("mvs_refine_d: bad arguments");
+  if (p->struct_size != sizeof(mvs_refine_params))
+    return mvs::arg_fail("mvs_refine_d: struct_size != sizeof(mvs_refine_params) (caller built against another mvs.h)");
+  if (p->prescaled != 0 && p->prescaled != 1) return mvs::arg_fail("mvs_refine_d: prescaled must be 0 or 1");
   RC(upload_meta(c, a));
   int V = a->view_count;
   int mw = mvs::map_dim(W, S), mh = mvs::map_dim(H, S);
-  // pipeline::refine_depth_map, pipeline.cpp:164-166
-  float gamma_ = (float)(2.0 * std::pow((double)p->gamma, 2.0));
-  float alpha_ = (float)(2.0 * std::pow((double)p->alpha, 2.0));
-  int kernel_size = p->kernel_size / 2;
+  // pipeline::refine_depth_map, pipeline.cpp:164-166 (skipped when the caller
+  // passes the values do_refinement receives)
+  float gamma_ = p->prescaled ? p->gamma : (float)(2.0 * std::pow((double)p->gamma, 2.0));
+  float alpha_ = p->prescaled ? p->alpha : (float)(2.0 * std::pow((double)p->alpha, 2.0));
+  int kernel_size = p->prescaled ? p->kernel_size : p->kernel_size / 2;
   int nks = p->kernel_step;
   if (nks <= 0) return mvs::arg_fail("mvs_refine_d: kernel_step must be > 0");
   int kss_i = kernel_size / nks * S;

@@ -220,7 +220,23 @@ __device__ __forceinline__ float slic_dist2(float4 px, int y, int x, float4 c, f
 // A workgroup assigns a 64 x 16 pixel block; the centres of every cell that
 // can be a candidate of its pixels (one cell around the block's cells) are
 // staged in LDS once, so the per-pixel candidate reads are LDS broadcasts.
+// S3 = false: the reference's active candidate loop (clcode.cl:474-494: the
+// 2x2 cells toward the pixel, x/y deltas swapped); S3 = true: the 3x3 loop the
+// reference keeps behind its comment switch (clcode.cl:496-516), the one its
+// kept Beer-Garden depth outputs were run with.
+template <bool S3>
+__device__ __forceinline__ void slic_cand(int ii, int jj, int dX, int dY, int& ox, int& oy) {
+  if (S3) {  // i over y outer, j over x inner
+    ox = jj - 1;
+    oy = ii - 1;
+  } else {  // i spans the x delta but offsets y (Appendix A #2)
+    ox = jj - 1 + dY;
+    oy = ii - 1 + dX;
+  }
+}
+
 constexpr int AS_TW = 64, AS_TH = 16, AS_MAXC = 128;
+template <bool S3>
 __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, const float* __restrict__ spixl,
                                                 int W, int H, int S, int mw, int mh, float xy_n, float col_n,
                                                 float weight, uint32_t* __restrict__ labels) {
@@ -267,11 +283,14 @@ __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, 
     // near tie needs the two correctly rounded square roots compared.
     float best2 = 0.0f, min_id = -1.0f;
     bool have = false;
+    constexpr int NC = S3 ? 3 : 2;
 #pragma unroll
-    for (int ii = 0; ii < 2; ii++)
+    for (int ii = 0; ii < NC; ii++)
 #pragma unroll
-      for (int jj = 0; jj < 2; jj++) {  // i spans the x delta but offsets y (Appendix A #2)
-        const int cx = cxg + (jj - 1 + dY), cy = cyg + (ii - 1 + dX);
+      for (int jj = 0; jj < NC; jj++) {
+        int ox, oy;
+        slic_cand<S3>(ii, jj, dX, dY, ox, oy);
+        const int cx = cxg + ox, cy = cyg + oy;
         const bool ok = cx >= 0 && cy >= 0 && cx < mw && cy < mh;
         const int e = ok ? (cy - cy0) * ncx + (cx - cx0) : 0;
         const float d2 = slic_dist2(px, row, col, cxyla[e], cbb[e], weight, xy_n, col_n);
@@ -411,11 +430,14 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
     const float n = acc[5];
     o[0] = (float)sp;
     if (n != 0) {
-      o[1] = acc[0] / n;
-      o[2] = acc[1] / n;
-      o[3] = acc[2] / n;
-      o[4] = acc[3] / n;
-      o[5] = acc[4] / n;
+      // x * RN(1/n): the reference device's division, as its kept overlays
+      // show (oracle orc_update)
+      const float r = 1.0f / n;
+      o[1] = acc[0] * r;
+      o[2] = acc[1] * r;
+      o[3] = acc[2] * r;
+      o[4] = acc[3] * r;
+      o[5] = acc[4] * r;
       o[6] = n;
     } else {
       o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
@@ -494,6 +516,7 @@ __global__ __launch_bounds__(256) void k_update_tiles(const float4* __restrict__
 // and, when part != nullptr, reduces the tile for each covering superpixel
 // exactly as k_update_tiles would from those labels -- one read of Lab per
 // SLIC iteration instead of two.
+template <bool S3>
 __global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__ lab,
                                                       const float* __restrict__ spixl, int W, int H, int S, int mw,
                                                       int mh, float xy_n, float col_n, float weight, int G, int cpl,
@@ -542,11 +565,13 @@ __global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__
     const int dX = divS(col + S / 2) - cxg, dY = divS(row + S / 2) - cyg;
     float best2 = 0.0f, min_id = -1.0f;
     bool have = false;
+    constexpr int NC = S3 ? 3 : 2;
 #pragma unroll
-    for (int ii = 0; ii < 2; ii++)
+    for (int ii = 0; ii < NC; ii++)
 #pragma unroll
-      for (int jj = 0; jj < 2; jj++) {  // i spans the x delta but offsets y (Appendix A #2), as k_assign
-        const int ox = jj - 1 + dY, oy = ii - 1 + dX;
+      for (int jj = 0; jj < NC; jj++) {  // the candidate order of k_assign
+        int ox, oy;
+        slic_cand<S3>(ii, jj, dX, dY, ox, oy);
         const int cx = cxg + ox, cy = cyg + oy;
         const bool ok = cx >= 0 && cy >= 0 && cx < mw && cy < mh;
         const int e = (oy + 1) * 3 + (ox + 1);
@@ -641,7 +666,7 @@ __global__ __launch_bounds__(256) void k_update_finalize(const float* __restrict
   } else if (c == 5) {
     o[6] = n;
   } else {
-    o[1 + c] = n != 0 ? acc / n : 0.0f;
+    o[1 + c] = n != 0 ? acc * (1.0f / n) : 0.0f;  // x * RN(1/n), as k_update
   }
 }
 
@@ -717,22 +742,22 @@ int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labe
 }
 
 int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
-                  float col_n, float weight, uint32_t* labels) {
+                  float col_n, float weight, int search, uint32_t* labels) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
   if ((AS_TW / S + 4) * (AS_TH / S + 4) > AS_MAXC) return arg_fail("SLIC assign: spixl_size too small");
-  hipLaunchKernelGGL(k_assign, dim3((W + AS_TW - 1) / AS_TW, (H + AS_TH - 1) / AS_TH, V), dim3(256), 0, s,
+  hipLaunchKernelGGL(search ? k_assign<true> : k_assign<false>, dim3((W + AS_TW - 1) / AS_TW, (H + AS_TH - 1) / AS_TH, V), dim3(256), 0, s,
                      (const float4*)lab, spixl, W, H, S, mw, mh, xy_n, col_n, weight, labels);
   MVS_LAUNCH_CHECK("k_assign");
   return 0;
 }
 
 int launch_assign_tiles(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
-                        float col_n, float weight, uint32_t* labels, float* part) {
+                        float col_n, float weight, int search, uint32_t* labels, float* part) {
   if (S % 16 != 0) return arg_fail("SLIC fused assign needs spixl_size % 16 == 0");
   int mw = map_dim(W, S), mh = map_dim(H, S);
   int G = (3 * S / kLocal) * (3 * S / kLocal), cpl = S * 3 / kLocal;
   int ntx = (W + 15) / 16, nty = (H + 15) / 16;
-  hipLaunchKernelGGL(k_assign_tiles, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, spixl, W,
+  hipLaunchKernelGGL(search ? k_assign_tiles<true> : k_assign_tiles<false>, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, spixl, W,
                      H, S, mw, mh, xy_n, col_n, weight, G, cpl, ntx, nty, labels, part);
   MVS_LAUNCH_CHECK("k_assign_tiles");
   return 0;

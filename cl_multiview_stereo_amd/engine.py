@@ -133,10 +133,11 @@ class Engine:
         return lab, l8
 
     def slic(self, lab: torch.Tensor, S: int, weight: float = 0.6, no_iter: int = 5, enforce_connectivity=False,
-             spixl=None, labels=None, edge_enable: int = 0):
+             spixl=None, labels=None, edge_enable: int = 0, search: int = 0):
         """mvs_slic_d.  edge_enable (include/mvs.h): 0 off, 1 the reference's
         apply_edge_values as it behaves (overwrites `lab` in place), 2 the
-        intended centre perturbation."""
+        intended centre perturbation.  search: 0 the reference's active 2x2
+        candidate loop, 1 the 3x3 loop behind its comment switch."""
         V, H, W, _ = lab.shape
         mw, mh = map_size(W, H, S)
         # s7 (disparity) is never written by the reference's SLIC (clcode.cl:285-293);
@@ -145,7 +146,8 @@ class Engine:
         labels = self.empty((V, H, W), torch.int32) if labels is None else labels
         if spixl.shape != (V, mh, mw, 8) or labels.shape != (V, H, W):
             raise ValueError("slic: output shapes do not match")
-        p = _lib.SlicParams(int(S), float(weight), int(no_iter), int(bool(enforce_connectivity)), int(edge_enable))
+        p = _lib.SlicParams(int(S), float(weight), int(no_iter), int(bool(enforce_connectivity)), int(edge_enable),
+                            int(search))
         self._stream()
         _lib.check(self.L.mvs_slic_d(self.ctx, _ptr(lab), V, W, H, C.byref(p), _ptr(spixl), _ptr(labels)),
                    "mvs_slic_d")

@@ -39,6 +39,7 @@ struct Settings {  // system_settings, clMVDE.cpp:14-36 defaults
   int no_iter = 5;
   bool enforce_connectivity = false;
   int edge_enable = 0;  // system_settings::edge_enable (header.h:61); 2 = the intended form (mvs.h)
+  int search = 0;       // mvs_slic_params::search: 1 = the 3x3 candidate loop (clcode.cl:496-516)
   int neib_hor = 1, neib_ver = 1;
   int min_disp = 30, max_disp = 60, inc = 1;
   float bl_ratio = 1.03590f;
@@ -53,7 +54,7 @@ struct Settings {  // system_settings, clMVDE.cpp:14-36 defaults
 int usage() {
   std::fprintf(stderr,
                "usage: mvs_cli --data LIST --array WxH [--spixl-size S] [--color-weight w] [--no-iter n]\n"
-               "               [--connectivity] [--edge | --edge-intended] [--min-disp a] [--max-disp b] [--inc i] [--neib-hor h]\n"
+               "               [--connectivity] [--edge | --edge-intended] [--search3x3] [--min-disp a] [--max-disp b] [--inc i] [--neib-hor h]\n"
                "               [--neib-ver v] [--bl-ratio r] [--kernel-size k] [--kernel-step s] [--fuse f]\n"
                "               [--gamma g] [--alpha a] [--no-prop p] [--final-state] [--filter] [--dump-init]\n"
                "               [--device d] [--out DIR] [--quiet]\n"
@@ -136,6 +137,7 @@ int main(int argc, char** argv) {
     else if (a == "--quiet") st.quiet = true;
     else if (a == "--edge") st.edge_enable = 1;  // edge_enable = true, as the reference behaves
     else if (a == "--edge-intended") st.edge_enable = 2;
+    else if (a == "--search3x3") st.search = 1;
     else if (!(v = val())) return usage();
     else if (a == "--data") st.data = v;
     else if (a == "--out") st.out = v;
@@ -205,7 +207,8 @@ int main(int argc, char** argv) {
   // ---- pipeline::perform_segmentation (pipeline.cpp:67-101) ----------------
   std::vector<float> lab(V * P * 4), spixl(V * M * 8, 0.0f);
   std::vector<uint32_t> labels(V * P);
-  mvs_slic_params sp{S, st.slic_color_weight, st.no_iter, st.enforce_connectivity ? 1 : 0, st.edge_enable};
+  mvs_slic_params sp{sizeof(mvs_slic_params), S, st.slic_color_weight, st.no_iter,
+                     st.enforce_connectivity ? 1 : 0, st.edge_enable, st.search};
   for (int v = 0; v < V; v++) {
     auto t0 = std::chrono::steady_clock::now();
     if (mvs_do_super_pixel_seg(ctx, imgs[v].rgbx.data(), W, H, &sp, &lab[v * P * 4], &spixl[v * M * 8],
@@ -236,8 +239,8 @@ int main(int argc, char** argv) {
   if (!st.quiet) std::printf("Time of initial depth estimation = %.3f ms\n", ms_since(t1));
 
   std::vector<float> disp(V * P);
-  mvs_refine_params rp{st.gamma, st.alpha, st.fuse, st.kernel_step, st.kernel_size, st.no_prop,
-                       st.fusion_compat ? 1 : 0};
+  mvs_refine_params rp{sizeof(mvs_refine_params), st.gamma, st.alpha, st.fuse, st.kernel_step, st.kernel_size,
+                       st.no_prop, st.fusion_compat ? 1 : 0, 0};
   auto t2 = std::chrono::steady_clock::now();
   if (mvs_do_refinement(ctx, W, H, S, spixl.data(), labels.data(), rep.data(), &arr, &rp, nullptr, disp.data()) !=
       MVS_OK)

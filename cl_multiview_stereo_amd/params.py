@@ -26,6 +26,9 @@ class Settings:
     no_iter: int = 5
     enforce_connectivity: bool = False
     edge_enable: bool = False
+    # find_center_association candidates: 0 the active 2x2 loop (clcode.cl:474-494),
+    # 1 the 3x3 loop behind the reference's comment switch (clcode.cl:496-516)
+    slic_search: int = 0
     num_disp_levels: int = 30
     neib_hor: int = 1
     neib_ver: int = 1

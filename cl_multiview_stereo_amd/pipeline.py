@@ -40,7 +40,8 @@ class SLIC:
         S = self.st.spixl_size
         if S == 1:
             return self.e.grid(lab, 1)
-        return self.e.slic(lab, S, self.st.slic_color_weight, self.st.no_iter, self.st.enforce_connectivity)
+        return self.e.slic(lab, S, self.st.slic_color_weight, self.st.no_iter, self.st.enforce_connectivity,
+                           search=self.st.slic_search)
 
 
 class PhotoConsistency:

@@ -48,8 +48,12 @@ enum {
 
 typedef struct mvs_ctx mvs_ctx;
 
-/* SLIC parameters: system_settings fields used by clSLIC (header.h:55-77). */
+/* SLIC parameters: system_settings fields used by clSLIC (header.h:55-77).
+ * ABI 0.3 (mvs_version): struct_size must be sizeof(mvs_slic_params) -- a
+ * caller built against an older mvs.h (0.1: four ints, no size field) is
+ * refused with MVS_E_ARG instead of having its fields misread. */
 typedef struct {
+  uint32_t struct_size;      /* = sizeof(mvs_slic_params) */
   int spixl_size;            /* S */
   float color_weight;        /* slic_color_weight (clMVDE.cpp:16 = 0.6) */
   int no_iter;               /* update/assign iterations (5) */
@@ -62,6 +66,12 @@ typedef struct {
                               *   pinned as zeros);
                               * 2 the intended path: Lab kept, each centre moves to its
                               *   least-edge 8-neighbour and takes its colour. */
+  int search;                /* candidate centres of find_center_association:
+                              * 0 the active loop (clcode.cl:474-494: 2x2 cells, x/y
+                              *   deltas swapped) -- the reference's default;
+                              * 1 the 3x3 loop behind the reference's comment switch
+                              *   (clcode.cl:496-516), with which its kept depth outputs
+                              *   were produced. */
 } mvs_slic_params;
 
 /* Camera array / hypothesis set (pipeline::perform_depth_est).  Its arrays are
@@ -77,15 +87,23 @@ typedef struct {
   const int32_t* subset_num; /* [V] */
 } mvs_array;
 
-/* Refinement parameters (system_settings; clDepthRefinement::do_refinement). */
+/* Refinement parameters (system_settings; clDepthRefinement::do_refinement).
+ * ABI 0.3: struct_size must be sizeof(mvs_refine_params). */
 typedef struct {
-  float gamma;               /* settings->gamma (2) */
-  float alpha;               /* settings->alpha (6) */
+  uint32_t struct_size;      /* = sizeof(mvs_refine_params) */
+  float gamma;               /* settings->gamma (2), or gamma' with prescaled = 1 */
+  float alpha;               /* settings->alpha (6), or alpha' with prescaled = 1 */
   float fuse;                /* settings->fuse (1) */
   int kernel_step;           /* settings->kernel_step (13) */
-  int kernel_size;           /* settings->kernel_size (1080) */
+  int kernel_size;           /* settings->kernel_size (1080), or its half with prescaled = 1 */
   int no_prop;               /* propagate iterations (5) */
   int fusion_compat;         /* 1: render current_state_dev as the reference does */
+  int prescaled;             /* 0: the library applies pipeline::refine_depth_map's derivation
+                              *    (pipeline.cpp:164-166: gamma' = 2 gamma^2, alpha' = 2 alpha^2,
+                              *    kernel_size / 2);
+                              * 1: gamma, alpha, kernel_size already are those values -- the
+                              *    arguments clDepthRefinement::do_refinement receives
+                              *    (depth_refinement.h:9), for a drop-in of that method */
 } mvs_refine_params;
 
 /* ---- context ----------------------------------------------------------- */

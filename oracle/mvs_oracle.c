@@ -129,8 +129,14 @@ static float slic_dist(const float* px, int y, int x, const float* c, float weig
   return sqrtf(d);
 }
 
-void orc_assign(const float* lab, const float* spixl, int W, int H, int S, float xy_n, float col_n,
-                float weight, uint32_t* labels) {
+/* search: 0 = the active candidate loop, clcode.cl:474-494 (2x2 cells, the
+ * x/y deltas swapped); 1 = the alternative the reference keeps behind its
+ * comment switch, clcode.cl:496-516 (the 3x3 cells around the pixel's cell,
+ * i over y outer, j over x inner).  The depth stages of the reference's kept
+ * Beer-Garden outputs (results/1- initialize disparity/initD_dev<k>.png,
+ * 7- propagate, 8- Fusion/fus4) were run with search 1. */
+void orc_assign_ex(const float* lab, const float* spixl, int W, int H, int S, float xy_n, float col_n,
+                   float weight, int search, uint32_t* labels) {
   int mw = orc_map_w(W, S), mh = orc_map_h(H, S);
 #pragma omp parallel for schedule(static)
   for (int row = 0; row < H; row++)
@@ -138,9 +144,11 @@ void orc_assign(const float* lab, const float* spixl, int W, int H, int S, float
       long pid = (long)row * W + col;
       int cxg = col / S, cyg = row / S;
       int dX = (col + S / 2) / S - cxg, dY = (row + S / 2) / S - cyg;
+      int ilo = search ? -1 : -1 + dX, ihi = search ? 1 : dX;
+      int jlo = search ? -1 : -1 + dY, jhi = search ? 1 : dY;
       float min_dist = 999999.9999f, min_id = -1;
-      for (int i = -1 + dX; i <= dX; i++)       /* i spans the x delta ... */
-        for (int j = -1 + dY; j <= dY; j++) {   /* ... but offsets y (swapped) */
+      for (int i = ilo; i <= ihi; i++)       /* i spans the x delta ... */
+        for (int j = jlo; j <= jhi; j++) {   /* ... but offsets y (swapped) */
           int cx = cxg + j, cy = cyg + i;
           if (cx >= 0 && cy >= 0 && cx < mw && cy < mh) {
             int ci = cy * mw + cx;
@@ -150,6 +158,11 @@ void orc_assign(const float* lab, const float* spixl, int W, int H, int S, float
         }
       labels[pid] = (uint32_t)min_id;
     }
+}
+
+void orc_assign(const float* lab, const float* spixl, int W, int H, int S, float xy_n, float col_n,
+                float weight, uint32_t* labels) {
+  orc_assign_ex(lab, spixl, W, H, S, xy_n, col_n, weight, 0, labels);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -196,8 +209,21 @@ void orc_update(const float* lab, const uint32_t* labels, int W, int H, int S, f
     o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
     float n = acc[5];
     if (n != 0) {
+#ifndef MVS_PROBE_IEEE_DIV
+      /* the centre means as x * RN(1/n), not x / n.  OpenCL 1.2 allows fp32
+       * division 2.5 ulp, and the reference's kept SLIC overlays show its
+       * device divided so: against results/blue_i<k>.png and
+       * "slic output/green<k>.png" this form leaves 492 and 412 boundary
+       * pixels of 31.0 M / 18.6 M differing where the IEEE quotient leaves
+       * 12,235 and 16,342 (tests/ref_artifacts.py).
+       * MVS_PROBE_IEEE_DIV (oracle/Makefile `probe`) keeps the IEEE quotient. */
+      float r = 1.0f / n;
+      o[1] = acc[0] * r; o[2] = acc[1] * r;
+      o[3] = acc[2] * r; o[4] = acc[3] * r; o[5] = acc[4] * r;
+#else
       o[1] = acc[0] / n; o[2] = acc[1] / n;
       o[3] = acc[2] / n; o[4] = acc[3] / n; o[5] = acc[4] / n;
+#endif
       o[6] = n;
     }
   }
@@ -329,8 +355,8 @@ void orc_slic(const uint8_t* rgbx, int W, int H, int S, float weight, int no_ite
   orc_slic_edge(rgbx, W, H, S, weight, no_iter, enforce_conn, 0, lab, spixl, labels);
 }
 
-void orc_slic_edge(const uint8_t* rgbx, int W, int H, int S, float weight, int no_iter, int enforce_conn,
-                   int edge_enable, float* lab, float* spixl, uint32_t* labels) {
+void orc_slic_ex(const uint8_t* rgbx, int W, int H, int S, float weight, int no_iter, int enforce_conn,
+                 int edge_enable, int search, float* lab, float* spixl, uint32_t* labels) {
   float xy = 1.0f / (1.4242f * (float)S);
   float col = 15.0f / (1.7321f * 128.0f);
   xy = xy * xy;
@@ -338,10 +364,10 @@ void orc_slic_edge(const uint8_t* rgbx, int W, int H, int S, float weight, int n
   orc_cvt(rgbx, W, H, lab);
   orc_init_centers(lab, W, H, S, spixl);
   orc_edge_step(lab, W, H, S, edge_enable, spixl);
-  orc_assign(lab, spixl, W, H, S, xy, col, weight, labels);
+  orc_assign_ex(lab, spixl, W, H, S, xy, col, weight, search, labels);
   for (int i = 0; i < no_iter; i++) {
     orc_update(lab, labels, W, H, S, spixl);
-    orc_assign(lab, spixl, W, H, S, xy, col, weight, labels);
+    orc_assign_ex(lab, spixl, W, H, S, xy, col, weight, search, labels);
   }
   if (enforce_conn) {
     uint32_t* tmp = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)W * H);
@@ -349,6 +375,11 @@ void orc_slic_edge(const uint8_t* rgbx, int W, int H, int S, float weight, int n
     orc_suppress(tmp, labels, W, H);
     free(tmp);
   }
+}
+
+void orc_slic_edge(const uint8_t* rgbx, int W, int H, int S, float weight, int no_iter, int enforce_conn,
+                   int edge_enable, float* lab, float* spixl, uint32_t* labels) {
+  orc_slic_ex(rgbx, W, H, S, weight, no_iter, enforce_conn, edge_enable, 0, lab, spixl, labels);
 }
 
 /* SLIC-off grid mode: cvt + init_cluster_centers + init_label_per_pixl */

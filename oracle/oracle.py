@@ -72,7 +72,7 @@ def l8(lab):
     return out
 
 
-def slic(rgbx, S, weight=0.6, no_iter=5, enforce_connectivity=False, edge_enable=0):
+def slic(rgbx, S, weight=0.6, no_iter=5, enforce_connectivity=False, edge_enable=0, search=0):
     """clSLIC::do_super_pixel_seg for ONE view -> (lab, spixl, labels).
     edge_enable: 0 off, 1 the reference's apply_edge_values as it behaves
     (Lab overwritten by the edge magnitude), 2 the intended form (centres moved
@@ -83,8 +83,8 @@ def slic(rgbx, S, weight=0.6, no_iter=5, enforce_connectivity=False, edge_enable
     lab = np.zeros((H, W, 4), np.float32)
     sp = np.zeros((mh, mw, 8), np.float32)
     lb = np.zeros((H, W), np.uint32)
-    lib().orc_slic_edge(_p(rgbx, u8p), W, H, S, _f(weight), no_iter, int(bool(enforce_connectivity)),
-                        int(edge_enable), _p(lab, f32p), _p(sp, f32p), _p(lb, u32p))
+    lib().orc_slic_ex(_p(rgbx, u8p), W, H, S, _f(weight), no_iter, int(bool(enforce_connectivity)),
+                      int(edge_enable), int(search), _p(lab, f32p), _p(sp, f32p), _p(lb, u32p))
     return lab, sp, lb
 
 
@@ -106,7 +106,7 @@ def init_centers(lab, S):
     return sp
 
 
-def assign(lab, spixl, S, weight=0.6):
+def assign(lab, spixl, S, weight=0.6, search=0):
     lab = np.ascontiguousarray(lab, np.float32)
     spixl = np.ascontiguousarray(spixl, np.float32)
     H, W = lab.shape[:2]
@@ -114,7 +114,8 @@ def assign(lab, spixl, S, weight=0.6):
     xy = f(1.0) / (f(1.4242) * f(S))
     col = f(15.0) / (f(1.7321) * f(128.0))
     lb = np.zeros((H, W), np.uint32)
-    lib().orc_assign(_p(lab, f32p), _p(spixl, f32p), W, H, S, _f(xy * xy), _f(col * col), _f(weight), _p(lb, u32p))
+    lib().orc_assign_ex(_p(lab, f32p), _p(spixl, f32p), W, H, S, _f(xy * xy), _f(col * col), _f(weight), int(search),
+                        _p(lb, u32p))
     return lb
 
 
@@ -292,13 +293,13 @@ def suppress(labels):
     return out
 
 
-def slic_from_lab(lab, S, weight=0.6, no_iter=5, enforce_connectivity=False):
+def slic_from_lab(lab, S, weight=0.6, no_iter=5, enforce_connectivity=False, search=0):
     """clSLIC::do_super_pixel_seg minus its cvt, on one view's Lab."""
     sp = init_centers(lab, S)
-    lb = assign(lab, sp, S, weight)
+    lb = assign(lab, sp, S, weight, search)
     for _ in range(no_iter):
         sp = update(lab, lb, S)
-        lb = assign(lab, sp, S, weight)
+        lb = assign(lab, sp, S, weight, search)
     if enforce_connectivity:
         lb = suppress(suppress(lb))
     return sp, lb

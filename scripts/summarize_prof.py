@@ -81,9 +81,22 @@ def main():
                   open(os.path.join(out, f"pmc_wta_{cfg}.json"), "w"), indent=1)
     ncc = [k for k in sorted(pmc) if k.startswith("k_ncc_volume") and "SQ_INSTS_VALU_per_launch" in pmc[k]]
     if ncc:
+        extra = {}
+        # the fused sweep runs several reference views per launch
+        # (mvs_ncc_wta_range_d): its VALU total over the pass divided by the
+        # views that pass's bench process swept (bench.py profile_counts)
+        try:
+            counts = json.load(open(os.path.join(src, "pmc_valu_bench.json")))["profile_counts"]
+            tot = sum(pmc[k]["SQ_INSTS_VALU_per_launch"] * pmc[k]["launches"] for k in ncc if k.endswith("true>"))
+            if counts.get("ncc_wta_views") and tot:
+                extra = {"fused_valu_wave_insts_per_view": tot / counts["ncc_wta_views"],
+                         "fused_views_in_pass": counts["ncc_wta_views"],
+                         "fused_launches_in_pass": sum(pmc[k]["launches"] for k in ncc if k.endswith("true>"))}
+        except (OSError, ValueError, KeyError):
+            pass
         json.dump({k: {"valu_wave_insts_per_launch": pmc[k]["SQ_INSTS_VALU_per_launch"],
                        "lds_wave_insts_per_launch": pmc[k].get("SQ_INSTS_LDS_per_launch"),
-                       "launches": pmc[k]["launches"]} for k in ncc} |
+                       "launches": pmc[k]["launches"]} for k in ncc} | extra |
                   {"source": f"profiles/{tag}_pmc.json", "note": "SQ_INSTS_VALU / SQ_INSTS_LDS, own --pmc pass",
                    "config": cfg, **shape},
                   open(os.path.join(out, f"pmc_ncc_{cfg}.json"), "w"), indent=1)

@@ -128,7 +128,7 @@ def update(lab, labels, S, local=16):
     n = acc[:, 5]
     nz = n != 0
     for c in range(5):
-        out[nz, 1 + c] = acc[nz, c] / n[nz]
+        out[nz, 1 + c] = acc[nz, c] * (f32(1) / n[nz])  # x * RN(1/n): DESIGN.md section 0
     out[nz, 6] = n[nz]
     return out.reshape(mh, mw, 8)
 

@@ -1,0 +1,299 @@
+#!/usr/bin/env python3
+"""Reconcile the oracle with the outputs the reference keeps in its tree.
+
+The reference has no tests; the only record of what its OpenCL path
+computed is the 8-bit PNGs under /root/reference/results/, written by its own
+plot functions from real camera-array images under /root/reference/Images/.
+This script re-renders each family the way the reference's writer does, from
+the oracle's output on the same decoded pixels, and scores the agreement over
+a documented grid of settings.  CPU only, container only (the reference tree
+does not exist on the GPU box); it lives under tests/ because it loads the
+oracle.  Writes profiles/r03_ref_artifacts.json.
+
+Renderers (reference file:line):
+  * SLIC overlay  -- clSLIC::draw_segmentation_lines, clSLIC.cpp:447-478: an
+    interior pixel (1..H-2, 1..W-2) is painted when its label differs from one
+    of its 4 neighbours, else copied from the input; the border rows/columns
+    are never written (the overlays hold MSVC's 0xCD fill there) and are not
+    scored.  The reference mask is "overlay pixel != input pixel".
+  * seed plot     -- clPhotoConsistency::img_translate, photo_consistency.cpp:414-437:
+    floor((s7 - 30) / 30 * 255) of the pixel's superpixel.
+  * state plot    -- clDepthRefinement::img_translate_state, depth_refinement.cpp:1498-1553
+    (element 0, range 30..60), written after propagate iteration 4 (:804-809).
+  * fusion plot   -- plot_full_image, depth_refinement.cpp:1473-1495, of the
+    fused disparity (spixl_to_image of current_state_dev, :1352).
+  * flatness plot -- img_translate_flatness, depth_refinement.cpp:299-322: ceil(fl.s0 * 255).
+  An 8-bit store of an out-of-range value is taken modulo 256 (MSVC x64
+  converts through a 32-bit integer).
+
+Settings grid (SLIC): candidate search (0 = the active 2x2 loop,
+clcode.cl:474-494; 1 = the 3x3 loop behind the comment switch at :496-516),
+no_iter, enforce_connectivity, colour weight; S = 8 (main(), clMVDE.cpp:15).
+Numerical variants: the pinned oracle (SLIC centre means as x * RN(1/n)), the
+contracting build (clang -ffp-contract=on -mfma, oracle/Makefile `contract`)
+and the IEEE-quotient probe (`probe`: x / n, this build's definition before
+round 3).
+
+    python tests/ref_artifacts.py [--quick]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from cl_multiview_stereo_amd import params  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+REF = "/root/reference"
+BUILDS = {"pinned": orc.LIB_PATH,
+          "contract": os.path.join(ROOT, "oracle", "_build", "liboracle_contract.so"),
+          "ieeediv": os.path.join(ROOT, "oracle", "_build", "liboracle_ieeediv.so")}
+F32 = np.float32
+
+# input sets: the 5x3 array (Images/c<k>f1.png) and the 3x3 Beer-Garden array
+C_SCENE = [f"Images/c{k}f1.png" for k in range(15)]
+BEER = [f"Images/Beer-Garden/img{k}.png" for k in range(9)]
+OVERLAYS = [  # family, input set, overlay path pattern
+    ("blue", C_SCENE, "results/blue{k}.png"),
+    ("blue_i", C_SCENE, "results/blue_i{k}.png"),
+    ("con_i", C_SCENE, "results/slic output/con_i{k}.png"),
+    ("green", BEER, "results/slic output/green{k}.png"),
+    ("green_new", BEER, "results/slic output/green_new{k}.png"),
+    ("green_new_2", BEER, "results/slic output/green_new_2{k}.png"),
+]
+
+
+def use(build):
+    orc._lib = C.CDLL(BUILDS[build])
+
+
+def load_rgb(rel):
+    from PIL import Image  # container-only dependency of this script
+    return np.array(Image.open(os.path.join(REF, rel)).convert("RGB"))
+
+
+def load_gray(rel):
+    from PIL import Image
+    a = np.array(Image.open(os.path.join(REF, rel)))
+    return a if a.ndim == 2 else a[..., 0]
+
+
+def rgbx_of(rgb):
+    out = np.zeros(rgb.shape[:2] + (4,), np.uint8)
+    out[..., :3] = rgb  # loadImageIn, file_handler.cpp:6-14: s0 = R
+    return out
+
+
+def boundary_mask(labels):
+    """draw_segmentation_lines' test, clSLIC.cpp:458-461 (interior only)."""
+    lb = labels.astype(np.int64)
+    m = np.zeros(lb.shape, bool)
+    c = lb[1:-1, 1:-1]
+    m[1:-1, 1:-1] = (c != lb[1:-1, 2:]) | (c != lb[1:-1, :-2]) | (c != lb[:-2, 1:-1]) | (c != lb[2:, 1:-1])
+    return m
+
+
+def overlay_mask(overlay, rgb):
+    return ~(overlay == rgb).all(-1)
+
+
+INNER = np.s_[1:-1, 1:-1]
+
+
+def plot8(d, lo=30.0, hi=60.0):
+    v = np.floor(((d.astype(F32) - F32(lo)) / (F32(hi) - F32(lo))) * F32(255))
+    return (v.astype(np.int64) % 256).astype(np.uint8)
+
+
+def per_pixel(spixl_field, labels):
+    return spixl_field.reshape(-1)[labels.astype(np.int64)].reshape(labels.shape)
+
+
+# ---------------------------------------------------------------------------
+def score_overlays(quick):
+    out = {}
+    grid = [(s, it, conn, w) for s in (0, 1) for it in ((1, 5) if quick else (0, 1, 2, 3, 5))
+            for conn in (0, 1) for w in ((0.6,) if quick else (0.6, 0.3, 1.0))]
+    for fam, inputs, pat in OVERLAYS:
+        rgb0 = load_rgb(inputs[0])
+        ref0 = overlay_mask(load_rgb(pat.format(k=0)), rgb0)
+        use("pinned")
+        res = []
+        for s, it, conn, w in grid:
+            _, _, lb = orc.slic(rgbx_of(rgb0), 8, w, it, conn, search=s)
+            mism = int(np.count_nonzero(boundary_mask(lb)[INNER] != ref0[INNER]))
+            res.append({"search": s, "no_iter": it, "connectivity": conn, "weight": w,
+                        "view0_mismatch_px": mism, "view0_agreement": 1 - mism / ref0[INNER].size})
+        res.sort(key=lambda r: r["view0_mismatch_px"])
+        best = res[0]
+        views = range(len(inputs)) if not quick else range(min(3, len(inputs)))
+        per_build = {}
+        for build in ("pinned", "contract", "ieeediv"):
+            use(build)
+            per = []
+            for k in views:
+                rgb = load_rgb(inputs[k])
+                ref = overlay_mask(load_rgb(pat.format(k=k)), rgb)
+                _, _, lb = orc.slic(rgbx_of(rgb), 8, best["weight"], best["no_iter"], best["connectivity"],
+                                    search=best["search"])
+                per.append(int(np.count_nonzero(boundary_mask(lb)[INNER] != ref[INNER])))
+            n = len(per) * ref0[INNER].size
+            per_build[build] = {"mismatch_px_per_view": per, "mismatch_px": sum(per),
+                                "agreement": 1 - sum(per) / n}
+        use("pinned")
+        out[fam] = {"inputs": inputs[0].rsplit("/", 1)[0] + "/", "overlay": pat, "views": len(list(views)),
+                    "reference_overlay_fraction": float(ref0[INNER].mean()),
+                    "best_setting": {k: best[k] for k in ("search", "no_iter", "connectivity", "weight")},
+                    "best_all_views": per_build, "grid_view0": res[:8]}
+        print(f"[overlay] {fam}: best {out[fam]['best_setting']} -> "
+              f"{per_build['pinned']['mismatch_px']} px of {n} ({per_build['pinned']['agreement']:.7f})", flush=True)
+    return out
+
+
+# ---------------------------------------------------------------------------
+def beer_garden_stack(search, build="pinned"):
+    use(build)
+    st = params.Settings()  # main()'s defaults: 3x3, S 8, levels 30..60, bl 1.0359
+    labs, sps, lbs = [], [], []
+    for k in range(9):
+        lab, sp, lb = orc.slic(rgbx_of(load_rgb(BEER[k])), st.spixl_size, st.slic_color_weight, st.no_iter,
+                               st.enforce_connectivity, search=search)
+        labs.append(lab)
+        sps.append(sp)
+        lbs.append(lb)
+    lab, sp, lb = np.stack(labs), np.stack(sps), np.stack(lbs)
+    rep = orc.boundary(sp, lb, st.spixl_size)
+    levels = params.disparity_levels(st.min_disp, st.max_disp, st.inc)
+    vs, sn = params.flatten_subsets(params.neighbour_lists(st.array_width, st.array_height, st.neib_hor,
+                                                           st.neib_ver))
+    sp = orc.sweep(lab, sp, rep, levels, vs, sn, st.array_width, st.bl_ratio, st.spixl_size)
+    return dict(lab=lab, spixl=sp, labels=lb, rep=rep, vs=vs, sn=sn, st=st)
+
+
+def purity(labels, plot):
+    """Fraction of pixels whose grey equals the most common grey of their
+    superpixel: 1.0 iff the plot is constant on every superpixel of `labels`."""
+    key = labels.astype(np.int64) * 256 + plot
+    u, c = np.unique(key, return_counts=True)
+    best = np.zeros(int(labels.max()) + 1, np.int64)
+    np.maximum.at(best, u // 256, c)
+    return float(best.sum() / plot.size)
+
+
+def reference_seeds(spixl, labels):
+    """The reference's own seeds, read back from initD_dev<k>.png: the plot is
+    injective on the integer levels 30..60, and constant on each superpixel."""
+    levels = np.arange(30, 61, dtype=F32)
+    grey = plot8(levels)
+    inv = {int(g): float(l) for g, l in zip(grey, levels)}
+    sp = spixl.copy()
+    changed = 0
+    for k in range(sp.shape[0]):
+        g = load_gray(f"results/1- initialize disparity/initD_dev{k}.png").astype(np.int64)
+        lb = labels[k].astype(np.int64)
+        key = lb * 256 + g
+        u, c = np.unique(key, return_counts=True)
+        order = np.lexsort((-c, u // 256))
+        u = u[order]
+        first = np.unique(u // 256, return_index=True)[1]
+        ids, gv = u[first] // 256, u[first] % 256
+        flat = sp[k].reshape(-1, 8)
+        new = np.array([inv.get(int(x), np.nan) for x in gv], F32)
+        ok = ~np.isnan(new)
+        changed += int(np.count_nonzero(flat[ids[ok], 7] != new[ok]))
+        flat[ids[ok], 7] = new[ok]
+    return sp, changed
+
+
+def score_depth(quick):
+    out = {}
+    stacks = {}
+    for search in (0, 1):
+        t0 = time.time()
+        b = beer_garden_stack(search)
+        stacks[search] = b
+        eq, pur = [], []
+        for k in range(9):
+            ref = load_gray(f"results/1- initialize disparity/initD_dev{k}.png")
+            ours = plot8(per_pixel(b["spixl"][k][..., 7], b["labels"][k]))
+            eq.append(float((ours == ref).mean()))
+            pur.append(purity(b["labels"][k], ref))
+        out[f"seeds_search{search}"] = {"plot": "results/1- initialize disparity/initD_dev<k>.png",
+                                        "equal_frac_per_view": eq, "equal_frac": float(np.mean(eq)),
+                                        "reference_plot_constant_on_our_superpixels": float(np.mean(pur)),
+                                        "seconds": time.time() - t0}
+        print(f"[seeds] search {search}: equal {np.mean(eq):.5f}, purity {np.mean(pur):.5f}", flush=True)
+    b = stacks[1]
+    st = b["st"]
+    ref_sp, changed = reference_seeds(b["spixl"], b["labels"])
+    for seeds, sp in (("ours", b["spixl"]), ("reference", ref_sp)):
+        for build in (("pinned",) if quick else ("pinned", "contract")):
+            use(build)
+            r = orc.refine(sp, b["labels"], b["rep"], b["vs"], b["sn"], st.array_width, st.bl_ratio, st.spixl_size,
+                           st.gamma, st.alpha, st.fuse, st.kernel_step, st.kernel_size, st.no_prop)
+            it4, fus = [], []
+            for k in range(9):
+                g = load_gray(f"results/7- propagate/change6_alter1 {k}.png")
+                it4.append(float((plot8(per_pixel(r["states"][4][k][..., 0], b["labels"][k])) == g).mean()))
+                f = load_gray(f"results/8- Fusion/fus4 {k}.png")
+                fus.append(float((plot8(r["disp"][k]) == f).mean()))
+            out[f"refine_{seeds}_seeds_{build}"] = {
+                "state_iter4_plot_equal_frac": float(np.mean(it4)), "per_view_state_iter4": it4,
+                "fus4_plot_equal_frac": float(np.mean(fus)), "per_view_fus4": fus}
+            print(f"[refine] {seeds} seeds, {build}: iter-4 state {np.mean(it4):.4f}, fus4 {np.mean(fus):.4f}",
+                  flush=True)
+    out["reference_seeds_changed"] = changed
+    out["superpixels"] = int(b["spixl"][..., 7].size)
+    use("pinned")
+    return out
+
+
+def score_flatness(quick):
+    out = {}
+    ks = range(3) if quick else range(15)
+    for search in (0, 1):
+        eq, w1 = [], []
+        for k in ks:
+            _, sp, lb = orc.slic(rgbx_of(load_rgb(C_SCENE[k])), 8, search=search)
+            fl = orc.flatness(sp[None], 1.0 / 8.0)[0]  # gamma' = 2 * 2^2 (pipeline.cpp:164), 1/gamma' (:130)
+            ours = (np.ceil(per_pixel(fl[..., 0], lb) * F32(255)).astype(np.int64) % 256)
+            ref = load_gray(f"results/2- flatness/flatness_new {k}.png").astype(np.int64)
+            eq.append(float((ours == ref).mean()))
+            w1.append(float((np.abs(ours - ref) <= 1).mean()))
+        out[f"search{search}"] = {"equal_frac": float(np.mean(eq)), "within_1_frac": float(np.mean(w1)),
+                                  "views": len(list(ks))}
+        print(f"[flatness] search {search}: equal {np.mean(eq):.4f}, within 1 {np.mean(w1):.4f}", flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="fewer views and settings (about a minute)")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03_ref_artifacts.json"))
+    a = ap.parse_args()
+    if not os.path.isdir(REF):
+        sys.exit("ref_artifacts: /root/reference is absent (container-only script)")
+    for b, path in BUILDS.items():
+        if not os.path.exists(path):
+            os.system(f"make -s -C {os.path.join(ROOT, 'oracle')} {'all' if b == 'pinned' else b}")
+    t0 = time.time()
+    res = {"what": "oracle vs the reference's kept PNG outputs (tests/ref_artifacts.py)",
+           "overlays": score_overlays(a.quick), "depth_beer_garden": score_depth(a.quick),
+           "flatness_c_scene": score_flatness(a.quick), "quick": a.quick}
+    res["seconds"] = time.time() - t0
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print("wrote", a.out)
+
+
+if __name__ == "__main__":
+    main()

@@ -90,6 +90,24 @@ def test_slic_edge(engine, name, mode):
         assert_bits(sp[v][..., :7], osp[..., :7], f"spixl v{v}")
 
 
+@pytest.mark.parametrize("no_iter", [0, 5])
+@pytest.mark.parametrize("name", ["c3x1_s8", "c5x1_s32", "c2x1_s40", "c2x2_s12"])
+def test_slic_search3x3(engine, name, no_iter):
+    """mvs_slic_params.search = 1: the 3x3 candidate loop behind the
+    reference's comment switch (clcode.cl:496-516), with which the reference's
+    kept depth outputs were produced.  Both assignment
+    paths (k_assign for S % 16 != 0, k_assign_tiles for S = 32)."""
+    c = CASES[name]
+    b = build(c)
+    lab, _ = engine.cvt(dev(b["stack"]))
+    sp, lb = engine.slic(lab, c["S"], 0.6, no_iter, search=1)
+    sp, lb = sp.cpu().numpy(), as_u32(lb)
+    for v in range(b["V"]):
+        _, osp, olb = orc.slic(b["stack"][v], c["S"], 0.6, no_iter, search=1)
+        assert_bits(lb[v], olb, f"labels v{v}")
+        assert_bits(sp[v][..., :7], osp[..., :7], f"spixl v{v}")
+
+
 @pytest.mark.parametrize("name", ["c3x1_s8", "c5x1_s32"])
 def test_slic_each_pass(engine, name):
     """Per-pass parity of the assign/update loop (no_iter = 0, 1, 2)."""

@@ -78,6 +78,7 @@ def parse(argv=None):
     ap.add_argument("--cost", default=None, choices=["ncc", "sad", "none"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sharded", action="store_true", help="skip the C4 view-sharded strong-scaling line")
+    ap.add_argument("--no-reference-cost", action="store_true", help="skip the C2 --cost sad sub-line")
     ap.add_argument("--two-pass", action="store_true",
                     help="headline = the two-pass step (cost volume in HBM + k_wta) instead of the fused sweep")
     ap.add_argument("--concurrent", action="store_true",
@@ -211,8 +212,15 @@ def _cpu_info():
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = None
+    quota = None
+    try:  # cgroup v2 CPU quota: "max 100000" or "<quota> <period>"
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = {"cpu.max": f"{q} {per}", "cpus": None if q == "max" else round(int(q) / int(per), 2)}
+    except (OSError, ValueError):
+        pass
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity,
-            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_quota": quota}
 
 
 def _pmc_traffic(name, W, H, D):
@@ -449,6 +457,13 @@ def bench(args, world, rank, local):
                                  "what": f"H2D of the {stack.nbytes / 1e6:.1f} MB RGBx stack (pinned) + the step "
                                          f"+ D2H of the {host_out.numel() * 4 / 1e6:.1f} MB disparity maps"}
 
+    # the reference's own arithmetic (SAD over Lab, clcode.cl:1030-1053) on the
+    # headline shape: the only cost against which the north star's L1 target
+    # is defined (C2 with --cost sad, 3 steps)
+    if args.config == "c2" and cost == "ncc" and world == 1 and not args.no_reference_cost:
+        res["reference_cost"] = reference_cost(args, e, st, stack, rgbx, cfg, world, sync,
+                                               check=rank == 0 and not args.no_cpu_baseline)
+
     # C4: one 32-view array sharded by reference view over the N GPUs (strong scaling)
     if not args.no_sharded and args.config in ("c2",) and cost == "ncc":
         res["view_sharded"] = view_sharded(args, e, world, rank, sync)
@@ -459,6 +474,42 @@ def bench(args, world, rank, local):
         except Exception as ex:  # report, never hide
             res["cpu_baseline"] = {"error": repr(ex)}
     return res
+
+
+def reference_cost(args, e, st, stack, rgbx, cfg, world, sync, check=True):
+    """C2 with the reference's SAD cost (initial_depth_estimation_v2 at S = 1,
+    the per-pixel k_sad_band sweep) instead of the build-defined NCC: 3 timed
+    steps after 1 warmup, and the depth L1 against the oracle on rows
+    0..61 of every reference view (a 64-row band; with horizontal-only
+    neighbours those rows equal the full image's: about 1 s of CPU)."""
+    import dataclasses
+
+    import torch
+
+    from cl_multiview_stereo_amd.pipeline import Pipeline
+    W, H = cfg["W"], cfg["H"]
+    V = stack.shape[0]
+    sst = dataclasses.replace(st, cost="sad")
+    p = Pipeline(e, sst, W, H, pixel_cost="sad", refine=False, filt=False, fused=False)
+    steps = 3
+    el, out = timed(lambda: p.exe_pipeline(rgbx), steps, 1, e.device, world, sync)
+    r = {"what": "the C2 step with the reference's cost (SAD over Lab, 5x5 sparse window, min over neighbours, "
+                 "WTA; clcode.cl:972-1069 at S = 1) in place of NCC 5x5",
+         "value": round(V * W * H * steps / el / 1e6, 3), "unit": "Mpix/s", "ms_per_step": round(el * 1e3 / steps, 4),
+         "steps": steps, "dtype": "f32"}
+    if check:
+        from oracle import oracle as orc
+        cam = p.cam
+        rows, keep = 64, 62
+        t0 = time.perf_counter()
+        lab_band = orc.cvt(np.ascontiguousarray(stack[:, :rows]))
+        want = orc.sweep_pixel_sad(lab_band, cam.levels, cam.view_subset, cam.subset_num, cfg["aw"], cfg["bl"])
+        got = out.disp.cpu().numpy()[:, :keep]
+        r["depth_l1_vs_oracle"] = {"value": float(np.abs(got - want[:, :keep]).mean()),
+                                   "bit_exact": bool(np.array_equal(got, want[:, :keep])),
+                                   "sample": f"rows 0..{keep - 1} of all {V} reference views, {W} wide "
+                                             f"(oracle: {time.perf_counter() - t0:.1f} s on the host)"}
+    return r
 
 
 def view_sharded(args, e, world, rank, sync):

@@ -182,7 +182,8 @@ class ShardedPipeline:
         S = st.spixl_size
         need = self.cam.views_needed(z0, z1)
         lab, l8 = b.cvt(rgbx, need)
-        sp_blk, lb_blk = b.slic(lab[z0:z1], S, st.slic_color_weight, st.no_iter, st.enforce_connectivity)
+        sp_blk, lb_blk = b.slic(lab[z0:z1], S, st.slic_color_weight, st.no_iter, st.enforce_connectivity,
+                                st.slic_search)
         spixl = _expand(sp_blk, V, z0)
         labels = _expand(lb_blk, V, z0)
         # the labels (4 B/px/view, the largest gather) are read from other views
@@ -275,10 +276,10 @@ class EngineBackend:
         l8 = self.e.empty((V, H, W), torch.uint8)
         return self.e.cvt_views(rgbx, views, lab, l8)
 
-    def slic(self, lab_blk, S, weight, no_iter, conn):
+    def slic(self, lab_blk, S, weight, no_iter, conn, search=0):
         if S == 1:
             return self.e.grid(lab_blk, 1)
-        return self.e.slic(lab_blk, S, weight, no_iter, conn)
+        return self.e.slic(lab_blk, S, weight, no_iter, conn, search=search)
 
     def boundary(self, spixl, labels, S, z0, z1):
         rep = torch.zeros(tuple(spixl.shape[:3]) + (8,), dtype=torch.uint8, device=self.e.device)

@@ -25,49 +25,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from cl_multiview_stereo_amd import params, synth  # noqa: E402
-from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather, all_blocks  # noqa: E402
+from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather  # noqa: E402,F401
 from cl_multiview_stereo_amd.engine import CameraArray, Engine  # noqa: E402
-
-
-class RecordingGather(ViewGather):
-    def __init__(self, V):
-        super().__init__(V)
-        self.rec = []
-
-    def __call__(self, local, full=None):
-        out = super().__call__(local, full)
-        self.rec.append(out.clone())
-        return out
-
-
-class ReplayGather:
-    """Stands in for ViewGather(V) at (rank, world): no communication."""
-
-    def __init__(self, V, rank, world, rec):
-        self.V, self.rank, self.world, self.rec = V, rank, world, rec
-        self.blocks = all_blocks(V, world)
-        self.i = 0
-        self.bytes_in = 0
-
-    @property
-    def block(self):
-        return self.blocks[self.rank]
-
-    def start(self, local, full):
-        from cl_multiview_stereo_amd.distributed import PendingGather
-        return PendingGather(self(local, full))
-
-    def __call__(self, local, full=None):
-        z0, z1 = self.block
-        rec = self.rec[self.i % len(self.rec)]
-        self.i += 1
-        self.bytes_in += (rec.numel() - local.numel()) * rec.element_size()
-        if full is None:
-            full = rec.clone()
-        elif full.data_ptr() != rec.data_ptr():
-            full.copy_(rec)
-        full[z0:z1] = local
-        return full
+from tests.replay_gather import RecordingGather, ReplayGather  # noqa: E402
 
 
 def timed(fn, steps, warmup):

@@ -1,0 +1,50 @@
+"""Gathers for measuring / testing the view-sharded pipeline on ONE GPU.
+
+RecordingGather: ViewGather (world 1) that keeps every tensor it returns.
+ReplayGather: stands in for ViewGather at (rank, world) with no
+communication -- each gather returns the recorded world-1 tensor with the
+rank's freshly computed block written into it, so the rank reads exactly the
+neighbour data a real all-gather would deliver and does exactly its share of
+the work (scripts/c4_shard_sim.py, tests/test_gpu_c4.py)."""
+from cl_multiview_stereo_amd.distributed import ViewGather, all_blocks
+
+
+class RecordingGather(ViewGather):
+    def __init__(self, V):
+        super().__init__(V)
+        self.rec = []
+
+    def __call__(self, local, full=None):
+        out = super().__call__(local, full)
+        self.rec.append(out.clone())
+        return out
+
+
+class ReplayGather:
+    """Stands in for ViewGather(V) at (rank, world): no communication."""
+
+    def __init__(self, V, rank, world, rec):
+        self.V, self.rank, self.world, self.rec = V, rank, world, rec
+        self.blocks = all_blocks(V, world)
+        self.i = 0
+        self.bytes_in = 0
+
+    @property
+    def block(self):
+        return self.blocks[self.rank]
+
+    def start(self, local, full):
+        from cl_multiview_stereo_amd.distributed import PendingGather
+        return PendingGather(self(local, full))
+
+    def __call__(self, local, full=None):
+        z0, z1 = self.block
+        rec = self.rec[self.i % len(self.rec)]
+        self.i += 1
+        self.bytes_in += (rec.numel() - local.numel()) * rec.element_size()
+        if full is None:
+            full = rec.clone()
+        elif full.data_ptr() != rec.data_ptr():
+            full.copy_(rec)
+        full[z0:z1] = local
+        return full

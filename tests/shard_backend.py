@@ -26,9 +26,9 @@ class OracleBackend:
             q[v] = orc.l8(lab[v])
         return torch.from_numpy(lab), torch.from_numpy(q)
 
-    def slic(self, lab_blk, S, weight, no_iter, conn):
+    def slic(self, lab_blk, S, weight, no_iter, conn, search=0):
         lab = _np(lab_blk)
-        outs = [orc.slic_from_lab(lab[v], S, weight, no_iter, conn) for v in range(lab.shape[0])]
+        outs = [orc.slic_from_lab(lab[v], S, weight, no_iter, conn, search) for v in range(lab.shape[0])]
         sp = np.stack([o[0] for o in outs]) if outs else np.zeros((0,), np.float32)
         lb = np.stack([o[1] for o in outs]).view(np.int32)
         return torch.from_numpy(sp), torch.from_numpy(lb)

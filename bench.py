@@ -394,8 +394,6 @@ def bench(args, world, rank, local):
                 "valu_issue_frac": round(per_view["insts"] * vpc / t_f / VALU_PEAK, 4),
                 "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op",
                 "valu_source": per_view["source"]})
-    res["profile_counts"] = {"ncc_wta_calls": calls["fused"], "ncc_wta_views": calls["fused_views"],
-                             "ncc_volume_calls": calls["ncc"], "wta_calls": calls["wta"]}
 
     # the two-pass step (cost volume in HBM + k_wta), same protocol: the
     # north star's roofline is k_wta's read of that volume
@@ -473,6 +471,10 @@ def bench(args, world, rank, local):
             res["cpu_baseline"], res["depth_l1_vs_oracle"] = cpu_baseline(pipe, stack, cfg, cost, out)
         except Exception as ex:  # report, never hide
             res["cpu_baseline"] = {"error": repr(ex)}
+    # every sweep call this process made (warmup, timed, two-pass, PCIe and C4
+    # legs): a PMC pass of this same command divides its totals by these
+    res["profile_counts"] = {"ncc_wta_calls": calls["fused"], "ncc_wta_views": calls["fused_views"],
+                             "ncc_volume_calls": calls["ncc"], "wta_calls": calls["wta"]}
     return res
 
 

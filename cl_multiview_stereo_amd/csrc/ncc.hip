@@ -33,8 +33,9 @@
 //     neighbour's bands land while this one is computed;
 //   * per (level, neighbour) a lane walks its column: per band row two
 //     VOP3P v_dot4_i32_i8 extend one prefix-sum chain of the horizontal K-tap
-//     centred correlation (no accumulator copies), per output row one integer
-//     subtract + convert give Srp', and per PAIR of output rows one
+//     centred correlation (no accumulator copies; the chain starts at the
+//     bits of 1.5 * 2^23, so two prefix sums read as floats differ by exactly
+//     Srp': one float subtract per output row, no integer convert), and per PAIR of output rows one
 //     v_pk_mul_f32 + one v_pk_fma_f32 give x (rows 2m, 2m+1 of the stats
 //     plane are one 16-byte LDS read), then v_max_f32 per cell;
 //   * the chunk's costs are written once, 64-column coalesced rows.
@@ -263,6 +264,16 @@ __device__ __forceinline__ void read_stat_pairs(const u32x4* col, int r0, f32x4 
 // keeps every partial sum without the accumulator copies the VOP2 v_dot4c
 // form forces.  The Makefile builds this file with the dot6 feature (v_dot4c)
 // off, so the compiler selects the VOP3P form and still tracks its hazards.
+// the lane id, recomputed where it is used (volatile: never hoisted, so it is
+// never a long-lived value the register allocator would spill)
+__device__ __forceinline__ int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+constexpr int kMagicI = 0x4B400000;  // the bits of 12582912.0f = 1.5 * 2^23
+constexpr float kMagicF = 12582912.0f;
 __device__ __forceinline__ int dot4(unsigned a, unsigned b, int c) {
   return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
 }
@@ -343,6 +354,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   };
   float E[DPW][TH];
   float sr[TH];  // reference 1/sqrt(var) per output row (NaN: invalid window)
+  // FUSE: sr lives in LDS during the step loop (lane-major [64][TH], after
+  // the band buffers and the merge area), read back at each chunk's fold --
+  // 8 fewer long-lived VGPRs, so the loop needs no scratch reload (a VMEM
+  // load there waits behind the in-flight band LDS-DMA)
+  float* srl = (float*)(smem + 16 * (size_t)max(2 * nbuf, FUSE ? 3 * NW * TH * 64 / 4 : 0));
   float wv0[TH], wv1[TH];  // FUSE: this wave's smallest and second smallest cost per row
   int wi0[TH];             //       level of the smallest
   if (FUSE) {
@@ -368,9 +384,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
       const int dl = c * DC + wave + NW * j;
       if (dl >= a.D) break;
       if (FUSE) {
+        float srv[TH];
+        {
+          const int ln = lane_now();
+#pragma unroll
+          for (int o = 0; o < TH; o += 4) {
+            const f32x4 t = *(const f32x4*)(srl + ln * TH + o);
+            srv[o] = t.x;
+            srv[o + 1] = t.y;
+            srv[o + 2] = t.z;
+            srv[o + 3] = t.w;
+          }
+        }
 #pragma unroll
         for (int o = 0; o < TH; o += 2) {
-          const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{sr[o], sr[o + 1]};
+          const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{srv[o], srv[o + 1]};
           const f32x2 r = f32x2{1.0f, 1.0f} - f32x2{vmax(e.x, -1.0f), vmax(e.y, -1.0f)};
 #pragma unroll
           for (int h = 0; h < 2; h++) {
@@ -442,6 +470,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     sr[o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
     rsn[o >> 1][o & 1] = -(float)s1;
   }
+  if (FUSE && wave == 0) {
+#pragma unroll
+    for (int o = 0; o < TH; o += 4) *(f32x4*)(srl + lane * TH + o) = f32x4{sr[o], sr[o + 1], sr[o + 2], sr[o + 3]};
+  }
   __syncthreads();
 
   int n = 0, c = 0;
@@ -457,6 +489,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     const u32x4* npk = nbase + (t & 1) * nbuf;
     const u32x4* nst = npk + a.pk_pairs * BW;
+    const int ln = lane_now();
     int lvv[2 * DPW];  // one scalar load of this wave's level shifts for step t
 #pragma unroll
     for (int i = 0; i < 2 * DPW; i++) lvv[i] = rec[NW * t].lv[i];
@@ -467,25 +500,29 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
       const int colo = lvv[2 * j], rows = lvv[2 * j + 1];
       u32x2 pv[NR];
       if (EVEN)
-        read_rows<NR, BW, true>(npk + colo + lane, rows & 0xffff, pv);
+        read_rows<NR, BW, true>(npk + colo + ln, rows & 0xffff, pv);
       else
-        read_rows<NR, BW, false>(npk + colo + lane, rows & 0xffff, pv);
+        read_rows<NR, BW, false>(npk + colo + ln, rows & 0xffff, pv);
       // prefix sums over band rows of the horizontal K-tap centred correlation
+      // prefix sums biased by kMagic: as floats they are 1.5 * 2^23 + the sum
+      // (|sum| < 2^22), so a difference of two is the exact integer window sum
+      // as a float -- one v_sub_f32 per row instead of v_sub_u32 + v_cvt
       int ps[NR];
-      ps[0] = dot4(qlo[0], pv[0].x, dot4(qhi[0], pv[0].y, 0));
+      ps[0] = dot4(qlo[0], pv[0].x, dot4(qhi[0], pv[0].y, kMagicI));
 #pragma unroll
       for (int k = 1; k < NR; k++) ps[k] = dot4(qlo[k], pv[k].x, dot4(qhi[k], pv[k].y, ps[k - 1]));
       f32x4 sv[TH / 2];
       if (EVEN)
-        read_stat_pairs<TH, BW, true>(nst + colo + lane, rows >> 16, sv);
+        read_stat_pairs<TH, BW, true>(nst + colo + ln, rows >> 16, sv);
       else
-        read_stat_pairs<TH, BW, false>(nst + colo + lane, rows >> 16, sv);
+        read_stat_pairs<TH, BW, false>(nst + colo + ln, rows >> 16, sv);
 #pragma unroll
       for (int m = 0; m < TH / 2; m++) {
         const int o = 2 * m;
-        const int s0 = o > 0 ? ps[o + 2 * R] - ps[o - 1] : ps[2 * R];  // Srp' of rows o, o+1 (exact)
-        const int s1 = ps[o + 1 + 2 * R] - ps[o];
-        const f32x2 f = f32x2{(float)s0, (float)s1};
+        // Srp' of rows o, o+1 (exact)
+        const float f0 = __int_as_float(ps[o + 2 * R]) - (o > 0 ? __int_as_float(ps[o - 1]) : kMagicF);
+        const float f1 = __int_as_float(ps[o + 1 + 2 * R]) - __int_as_float(ps[o]);
+        const f32x2 f = f32x2{f0, f1};
         const f32x2 xv = __builtin_elementwise_fma(rsn[m], f32x2{sv[m].z, sv[m].w}, f * f32x2{sv[m].x, sv[m].y});
         E[j][o] = vmax(E[j][o], xv.x);
         E[j][o + 1] = vmax(E[j][o + 1], xv.y);
@@ -615,7 +652,7 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
   a.nch = (a.D + DC - 1) / DC;
   dim3 g(8 * a.tiles_per_xcd);
   auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, EVEN, false> : k_ncc_volume<K, TH, DPW, NW, BW, EVEN, true>;
-  if (!vol) lds = std::max(lds, (size_t)3 * 4 * NW * TH * 64);  // the waves' WTA partials
+  if (!vol) lds = std::max(lds, (size_t)3 * 4 * NW * TH * 64) + 4 * TH * 64;  // WTA partials; + s_r [64][TH]
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(ncc lds)");

@@ -251,7 +251,6 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
 // lexicographically at the end.
 constexpr int SB_TW = 60;   // output columns per tile
 constexpr int SB_ADW = 68;  // AD plane pitch (float2): lanes 60..63 read up to column 67
-constexpr int SB_RPW = 6;   // band rows per wave the prefetch holds (band rows <= 24)
 constexpr int SB_NBLK = 2;  // 64-column blocks per band row (band columns <= 128)
 constexpr float SB_INIT = 1000000.0f;
 // row-table entry of a row outside the image: a valid entry (yp-by0)*bw - bx0
@@ -341,34 +340,31 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
   float2* myad = adb + wave * RR * SB_ADW;
   const int T = a.nch * a.nn;
 
-  float4 pf[SB_RPW][SB_NBLK];
   SadBand pg{0, 0, 0, 0};
-  // global -> registers: step t's band, wave w holding rows w, w+4, ...
-  auto fetch = [&](int t) {
+  // step t's band into LDS buffer b by 16-byte LDS-DMA (lane l's pixel lands
+  // at 16 l past the wave-uniform row address), wave w taking rows w, w+4, ...
+  // No registers hold the band: the register-staged prefetch this replaces
+  // (12 float4 per lane) spilled to scratch, and the spill store waited for
+  // the prefetch loads before the step could compute.  Columns past the band
+  // (pitch a.bw is a multiple of 64) get a clamped copy nothing reads.
+  auto stage = [&](int t, int b) {
     const SadRec& e = plan[t];
     pg = sad_band_of<TH>(e, x0, y0, W, H);
     const float4* src = lab + (long)e.view * P + (long)pg.by0 * W + pg.bx0;
-#pragma unroll
-    for (int m = 0; m < SB_RPW; m++)
-#pragma unroll
-      for (int cb = 0; cb < SB_NBLK; cb++) {
-        const int i = wave + 4 * m, col = cb * 64 + lane;
-        if (i < pg.nrows && col < pg.ncols) pf[m][cb] = src[(long)i * W + col];
-      }
+    float4* dst = band + b * a.brows * a.bw;
+    const int nblk = (pg.ncols + 63) >> 6;
+    for (int cb = 0; cb < nblk; cb++) {
+      const int col = min(cb * 64 + lane, pg.ncols - 1);
+      for (int i = wave; i < pg.nrows; i += 4)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + (long)i * W + col),
+                                         (__attribute__((address_space(3))) void*)(dst + i * a.bw + cb * 64), 16, 0, 0);
+    }
   };
-  // registers -> LDS buffer b, and step t's row table: per (level j, region
-  // row r) the band index of row yp minus bx0 (so + xp gives the pixel), or
-  // SB_NOROW when the reference row or the projected row leaves the image
+  // step t's row table into buffer b: per (level j, region row r) the band
+  // index of row yp minus bx0 (so + xp gives the pixel), or SB_NOROW when the
+  // reference row or the projected row leaves the image
   auto commit = [&](int t, int b) {
     const SadRec& e = plan[t];
-    float4* dst = band + b * a.brows * a.bw;
-#pragma unroll
-    for (int m = 0; m < SB_RPW; m++)
-#pragma unroll
-      for (int cb = 0; cb < SB_NBLK; cb++) {
-        const int i = wave + 4 * m, col = cb * 64 + lane;
-        if (i < pg.nrows && col < pg.ncols) dst[i * a.bw + col] = pf[m][cb];
-      }
     int* tb = rtab + b * DC * RR;
     const int c = t / a.nn;
     for (int k = tid; k < DC * RR; k += 256) {
@@ -392,17 +388,19 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
   }
   f32x2 mn[PPW][TH];
   if (T > 0) {
-    fetch(0);
+    stage(0, 0);
     commit(0, 0);
   }
   __syncthreads();
   for (int t = 0; t < T; t++) {
     if (MODE == 1 && t > 0) {
-      fetch(t);
+      stage(t, t & 1);
       commit(t, t & 1);
       __syncthreads();
     }
-    if (MODE == 0 && t + 1 < T) fetch(t + 1);  // lands in registers while this step computes
+    // step t+1's band lands in the other buffer (last read in step t-1, before
+    // the previous barrier) while this step computes
+    if (MODE == 0 && t + 1 < T) stage(t + 1, (t + 1) & 1);
     const int c = t / a.nn, n = t - c * a.nn;
     if (n == 0) {
 #pragma unroll
@@ -508,8 +506,8 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
         }
       }
     }
-    // the prefetched band into the other buffer (last read in step t-1, before
-    // the previous barrier), then publish it
+    // step t+1's row table (its rows were last read in step t-1); the barrier
+    // (vmcnt(0) first) publishes the table and the landed band
     if (MODE == 0 && t + 1 < T) commit(t + 1, (t + 1) & 1);
     __syncthreads();
   }
@@ -853,12 +851,12 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
     }
   SadArgs a{};
   a.W = W; a.H = H; a.D = D; a.nn = nn; a.z = z; a.nch = nch;
-  a.bw = 64 + span_x;
+  a.bw = (64 + span_x + 63) & ~63;  // whole 64-pixel LDS-DMA pieces per band row
   a.brows = RR + (int)std::ceil(span_y) + 2;
   const size_t lds = 16 * 2 * (size_t)a.brows * a.bw + (SYS ? 0 : 8 * 4 * (size_t)RR * SB_ADW) +
                      4 * 2 * (size_t)DC * RR;
-  // the prefetch holds at most 4 * SB_RPW band rows of SB_NBLK * 64 columns
-  if (a.brows > 4 * SB_RPW || a.bw > 64 * SB_NBLK) return 1;
+  // band columns: SB_NBLK pieces of 64 at most (the systolic tile's reach)
+  if (a.bw > 64 * SB_NBLK) return 1;
   if (lds > 160 * 1024 || (size_t)4 * TH * 64 * 8 > 16 * 2 * (size_t)a.brows * a.bw) return 1;
   int rc = 0;
   const int32_t* dev = plan_upload(ctx, table, &rc);

@@ -140,6 +140,19 @@ class PendingGather:
         return self.full
 
 
+def _narrow_labels(g: ViewGather, spixl: torch.Tensor) -> bool:
+    """Gather the labels as 16-bit values: more than one rank, and every label
+    (< mw * mh) fits.  MVS_LABELS16=0 keeps the 32-bit gather (A/B)."""
+    mw_mh = spixl.shape[1] * spixl.shape[2]
+    return g.world > 1 and mw_mh <= 1 << 16 and os.environ.get("MVS_LABELS16", "1") != "0"
+
+
+def _bytes(t: torch.Tensor) -> torch.Tensor:
+    """A contiguous [n, ...] tensor as [n, bytes per view] uint8 (every
+    collective backend moves bytes, gloo included)."""
+    return t.view(torch.uint8).view(t.shape[0], -1)
+
+
 def _expand(blk: torch.Tensor, V: int, z0: int) -> torch.Tensor:
     """[V, ...] holding `blk` at views [z0, z0 + len(blk)); the other views are
     left unset (an all-gather fills them before any stage reads them)."""
@@ -186,16 +199,28 @@ class ShardedPipeline:
                                 st.slic_search)
         spixl = _expand(sp_blk, V, z0)
         labels = _expand(lb_blk, V, z0)
-        # the labels (4 B/px/view, the largest gather) are read from other views
-        # only by the refinement: in flight while this rank sweeps its block
-        pending = g.start(labels[z0:z1], labels)
+        # the labels (the largest gather) are read from other views only by the
+        # refinement: in flight while this rank sweeps its block.  With fewer
+        # than 2^16 superpixels per view they travel as 16-bit values (half the
+        # bytes over xGMI), widened after the wait.
+        narrow = _narrow_labels(g, spixl)
+        if narrow:
+            l16 = torch.empty(labels.shape, dtype=torch.int16, device=labels.device)
+            l16[z0:z1] = lb_blk.to(torch.int16)  # two's-complement wrap keeps the low 16 bits
+            pending = g.start(_bytes(l16[z0:z1]), _bytes(l16))
+        else:
+            pending = g.start(labels[z0:z1], labels)
         rep = b.boundary(spixl, labels, S, z0, z1)  # own block only
         b.sweep_spixl(lab, spixl, rep, self.cam, S, z0, z1)
         out = ShardOutput(z0, z1, spixl, labels)
         if self.pixel_cost:
             out.disp, out.conf = b.pixel_sweep(lab, l8, self.cam, z0, z1, self.pixel_cost, st.window, need)
         out.spixl = g(spixl[z0:z1], spixl)  # centres + seeds (s7) of every view
-        out.labels = pending.wait()
+        if narrow:
+            pending.wait()
+            out.labels = l16.to(torch.int32).bitwise_and_(0xFFFF)
+        else:
+            out.labels = pending.wait()
         spixl, labels = out.spixl, out.labels
         full = None
         if self.refine:

@@ -6,6 +6,8 @@ communication -- each gather returns the recorded world-1 tensor with the
 rank's freshly computed block written into it, so the rank reads exactly the
 neighbour data a real all-gather would deliver and does exactly its share of
 the work (scripts/c4_shard_sim.py, tests/test_gpu_c4.py)."""
+import torch
+
 from cl_multiview_stereo_amd.distributed import ViewGather, all_blocks
 
 
@@ -40,6 +42,10 @@ class ReplayGather:
     def __call__(self, local, full=None):
         z0, z1 = self.block
         rec = self.rec[self.i % len(self.rec)]
+        if rec.dtype == torch.int32 and local.dtype == torch.uint8:
+            # the world-1 run gathered the labels as int32; at world > 1 they
+            # travel as the bytes of their 16-bit values (distributed._narrow_labels)
+            rec = rec.to(torch.int16).view(torch.uint8).view(rec.shape[0], -1)
         self.i += 1
         self.bytes_in += (rec.numel() - local.numel()) * rec.element_size()
         if full is None:

@@ -149,3 +149,14 @@ def test_async_gather_gloo():
         want = np.concatenate([np.arange(20.0).reshape(4, 5) + 100 * r for r in range(2)]).astype(np.float32)
         for r in range(2):
             assert np.array_equal(np.load(os.path.join(d, f"g{r}.npy")), want)
+
+
+def test_labels_16bit_round_trip():
+    """The 16-bit labels gather (distributed._narrow_labels): int32 -> int16
+    (wrap) -> bytes -> int16 -> int32 & 0xFFFF is the identity on 0..65535."""
+    from cl_multiview_stereo_amd.distributed import _bytes
+    t = torch.arange(0, 1 << 16, dtype=torch.int32).view(4, 128, 128)
+    l16 = t.to(torch.int16)
+    b = _bytes(l16).clone()
+    back = b.view(torch.int16).view(4, 128, 128).to(torch.int32).bitwise_and_(0xFFFF)
+    assert torch.equal(back, t)

@@ -101,10 +101,11 @@ def test_sad_kernel_variants(engine, kind, monkeypatch):
 
 
 def test_sad_explicit_variant_does_not_fall_back(engine, monkeypatch):
-    """band8x2 cannot stage the 3x3 array's vertical 16-level bands: named
-    explicitly it fails loudly instead of running the gather kernel."""
+    """band8x2 cannot stage a neighbour 5 cameras away (16 levels x 5 px = 75
+    columns of shift: a band wider than its 128 columns): named explicitly it
+    fails loudly instead of running the gather kernel."""
     monkeypatch.setenv("MVS_SAD_KERNEL", "band8x2")
-    stack, _ = synth.make_stack(140, 50, 3, 3, 0, 20, 1.0359, 12)
+    stack, _ = synth.make_stack(140, 50, 6, 1, 0, 20, 1.0, 12)
     lab, _ = engine.cvt(torch.from_numpy(stack).cuda())
     with pytest.raises(Exception, match="cannot stage"):
-        engine.sweep_pixel_sad(lab, _cam(3, 3, 0, 20, 1, 1, 1.0359), 0, 9)
+        engine.sweep_pixel_sad(lab, _cam(6, 1, 0, 20, 5, 0, 1.0), 0, 6)

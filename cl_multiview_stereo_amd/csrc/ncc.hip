@@ -438,6 +438,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   if (T == 0) {  // no neighbours: every window invalid, cost 2
 #pragma unroll
     for (int o = 0; o < TH; o++) sr[o] = __int_as_float(0x7fc00000);
+    if (FUSE) {  // the fused store reads s_r from LDS
+      if (wave == 0)
+#pragma unroll
+        for (int o = 0; o < TH; o += 4) *(f32x4*)(srl + lane * TH + o) = f32x4{sr[o], sr[o + 1], sr[o + 2], sr[o + 3]};
+      __syncthreads();
+    }
     for (int c = 0; c < a.nch; c++) store(c);
   } else {
   stage(0, 0, 0);

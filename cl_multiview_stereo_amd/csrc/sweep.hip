@@ -290,9 +290,10 @@ __device__ __forceinline__ SadBand sad_band_of(const SadRec& e, int x0, int y0, 
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// wave_shr:1 -- lane l receives lane l-1's value (lane 0: 0)
+// wave_shr:1 -- lane l receives lane l-1's value (lane 0: 0 by bound_ctrl;
+// no `old` operand, so no zeroing move per shift)
 __device__ __forceinline__ float shr1(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 
 // MODE 0: register-staged band prefetch (default); 1: load + store the band at
@@ -305,7 +306,13 @@ __device__ __forceinline__ float shr1(float v) {
 // (DPP wave_shr:1, folded into the first add of each column): after the 5th
 // column, lane l holds the output of image column x0 + l - 4.  The AD plane,
 // its LDS writes/reads and the wave barriers of the two-phase form disappear.
-template <int TH, int PPW, int MODE, bool SYS = false>
+// AFF (SYS only): every level's row shift is integral, so region row r of
+// level j reads band row r + (y0 - 2 - fdy_j - by0) exactly and is valid on
+// one interval of r: the rows are addressed by immediate offsets r * BWT from
+// one per-level lane address, and validity is a scalar interval test -- no
+// row table reads, no per-row address arithmetic or compares.  BWT = the band
+// pitch (a.bw) as a compile-time constant (0: runtime, the table path).
+template <int TH, int PPW, int MODE, bool SYS = false, bool AFF = false, int BWT = 0>
 __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab, const float* __restrict__ levels,
                                                   const SadRec* __restrict__ plan, SadArgs a,
                                                   float* __restrict__ disp) {
@@ -419,6 +426,25 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
       const f32x2 k30 = f32x2{30.0f, 30.0f};
       // A. taps of the lane's region column, both levels
       f32x2 ad[RR];
+      if constexpr (AFF) {
+        const SadBand g = sad_band_of<TH>(e, x0, y0, W, H);  // this step's band (pg is step t+1's)
+        const int off0 = (int)e.fdy[j0], off1 = (int)e.fdy[j0 + 1];
+        const int rlo0 = max(max(0, 2 - y0), 2 - y0 + off0), rhi0 = min(min(RR - 1, H + 1 - y0), H + 1 - y0 + off0);
+        const int rlo1 = max(max(0, 2 - y0), 2 - y0 + off1), rhi1 = min(min(RR - 1, H + 1 - y0), H + 1 - y0 + off1);
+        const int b0 = xok0 ? (y0 - 2 - off0 - g.by0) * BWT + xp0 - g.bx0 : 0;
+        const int b1 = xok1 ? (y0 - 2 - off1 - g.by0) * BWT + xp1 - g.bx0 : 0;
+#pragma unroll
+        for (int r = 0; r < RR; r++) {
+          const bool v0 = xok0 && r >= rlo0 && r <= rhi0, v1 = xok1 && r >= rlo1 && r <= rhi1;
+          const float4 n0 = bnd[b0 + r * BWT], n1 = bnd[b1 + r * BWT];
+          asm volatile("" ::"v"(n0.w), "v"(n1.w));  // keep the full 16-B ds_read_b128
+          float d0 = fabsf(rL[r] - n0.x) + fabsf(ra[r] - n0.y);
+          d0 = d0 + fabsf(rb[r] - n0.z);
+          float d1 = fabsf(rL[r] - n1.x) + fabsf(ra[r] - n1.y);
+          d1 = d1 + fabsf(rb[r] - n1.z);
+          ad[r] = f32x2{v0 ? d0 : 30.0f, v1 ? d1 : 30.0f};
+        }
+      } else {
 #pragma unroll
       for (int r = 0; r < RR; r++) {
         const int t0 = tb[j0 * RR + r], t1 = tb[(j0 + 1) * RR + r];
@@ -431,6 +457,7 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
         d1 = d1 + fabsf(rb[r] - n1.z);
         ad[r] = f32x2{v0 ? d0 : 30.0f, v1 ? d1 : 30.0f};
         if (!SYS) myad[r * SB_ADW + lane] = make_float2(ad[r].x, ad[r].y);
+      }
       }
       if (SYS) {
         // B'. systolic: column 0 starts the chains (first tap: ((0+30)-30)+a = a
@@ -508,7 +535,7 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
     }
     // step t+1's row table (its rows were last read in step t-1); the barrier
     // (vmcnt(0) first) publishes the table and the landed band
-    if (MODE == 0 && t + 1 < T) commit(t + 1, (t + 1) & 1);
+    if (MODE == 0 && t + 1 < T && !AFF) commit(t + 1, (t + 1) & 1);
     __syncthreads();
   }
   // merge the 4 waves' winners: lexicographic (cost, level)
@@ -812,6 +839,7 @@ namespace {
 template <int TH, int PPW, int MODE = 0, bool SYS = false>
 int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
                       const int* vs_host, const int* sn_host, int aw, float bl, int z, float* disp) {
+  bool aff = SYS && MODE == 0 && getenv("MVS_SAD_AFF") == nullptr;  // MVS_SAD_AFF set: the table path (A/B)
   constexpr int RR = TH + 4, DC = 8 * PPW;
   const int nn = sn_host[z];
   const int nch = (D + DC - 1) / DC;
@@ -838,6 +866,7 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
         if (fdx != std::trunc(fdx) || std::fabs(fdx) > 1e6f) return 1;
         e.sx[j] = (int)fdx;
         e.fdy[j] = fdy;
+        if (fdy != std::trunc(fdy) || std::fabs(fdy) > 1e6f) aff = false;
         if (c * DC + j < D) {
           e.sxmin = std::min(e.sxmin, e.sx[j]);
           e.sxmax = std::max(e.sxmax, e.sx[j]);
@@ -865,6 +894,9 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
   a.ntiles = a.tiles_x * ((H + TH - 1) / TH);
   a.tiles_per_xcd = (a.ntiles + 7) / 8;
   auto kern = k_sad_band<TH, PPW, MODE, SYS>;
+  if constexpr (SYS && MODE == 0) {
+    if (aff) kern = a.bw == 64 ? k_sad_band<TH, PPW, MODE, SYS, true, 64> : k_sad_band<TH, PPW, MODE, SYS, true, 128>;
+  }
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(sad lds)");

@@ -100,6 +100,20 @@ def test_sad_kernel_variants(engine, kind, monkeypatch):
     assert os.environ["MVS_SAD_KERNEL"] == kind
 
 
+@pytest.mark.parametrize("table", [False, True])
+@pytest.mark.parametrize("aw,ah,nh,nv", [(3, 3, 1, 1), (5, 1, 4, 0), (4, 3, 2, 2)])
+def test_sad_affine_rows(engine, monkeypatch, aw, ah, nh, nv, table):
+    """The systolic kernel's affine band addressing (every row shift integral:
+    bl_ratio 1, whole levels; 64- and 128-column bands) against the row-table
+    path (MVS_SAD_AFF set) on the same geometry, vertical and diagonal
+    neighbours included."""
+    monkeypatch.setenv("MVS_SAD_KERNEL", "sys8")
+    if table:
+        monkeypatch.setenv("MVS_SAD_AFF", "0")
+    stack, _ = synth.make_stack(200, 60, aw, ah, 0, 19, 1.0, 21 + aw)
+    _check(engine, stack, _cam(aw, ah, 0, 19, nh, nv, 1.0), tag=f"aff {aw}x{ah} table={table}")
+
+
 def test_sad_explicit_variant_does_not_fall_back(engine, monkeypatch):
     """band8x2 cannot stage a neighbour 5 cameras away (16 levels x 5 px = 75
     columns of shift: a band wider than its 128 columns): named explicitly it

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
   f32x2 mn[PPW][TH];
   if (T > 0) {
     stage(0, 0);
-    commit(0, 0);
+    if (!AFF) commit(0, 0);
   }
   __syncthreads();
   for (int t = 0; t < T; t++) {
@@ -881,9 +881,12 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
   SadArgs a{};
   a.W = W; a.H = H; a.D = D; a.nn = nn; a.z = z; a.nch = nch;
   a.bw = (64 + span_x + 63) & ~63;  // whole 64-pixel LDS-DMA pieces per band row
-  a.brows = RR + (int)std::ceil(span_y) + 2;
+  // a step's band spans at most RR + ceil(span_y) rows (sad_band_of: the
+  // truncated ends differ by < RR + span_y); one spare row for the float
+  // rounding of fractional shifts, none when every shift is integral
+  a.brows = RR + (int)std::ceil(span_y) + (aff ? 0 : 1);
   const size_t lds = 16 * 2 * (size_t)a.brows * a.bw + (SYS ? 0 : 8 * 4 * (size_t)RR * SB_ADW) +
-                     4 * 2 * (size_t)DC * RR;
+                     (aff ? 0 : 4 * 2 * (size_t)DC * RR);
   // band columns: SB_NBLK pieces of 64 at most (the systolic tile's reach)
   if (a.bw > 64 * SB_NBLK) return 1;
   if (lds > 160 * 1024 || (size_t)4 * TH * 64 * 8 > 16 * 2 * (size_t)a.brows * a.bw) return 1;

@@ -153,7 +153,7 @@ void* scratch(mvs_ctx* ctx, size_t bytes, int* rc) {
 extern "C" {
 
 const char* mvs_last_error(void) { return g_err.c_str(); }
-const char* mvs_version(void) { return "mvs-mi355x 0.3 (gfx950)"; }
+const char* mvs_version(void) { return "mvs-mi355x 0.4 (gfx950)"; }
 
 int mvs_create(int device, mvs_ctx** out) {
   if (!out) return mvs::arg_fail("mvs_create: out is null");
@@ -446,15 +446,16 @@ int mvs_proj_inv_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ra
                    float* proj, int z0, int z1) {
   if (!c || !disp_full || !proj || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V || z0 > z1)
     return mvs::arg_fail("mvs_proj_inv_d: bad arguments");
-  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1, 0, H);
+  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1, 0, H, false);
 }
 
 int mvs_proj_inv_rows_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, const float* disp_full,
-                        float* proj, int z0, int z1, int y0, int y1) {
-  if (!c || !disp_full || !proj || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V || z0 > z1 ||
+                        float* proj, int proj_band, int z0, int z1, int y0, int y1) {
+  if (!c || !disp_full || (!proj && y1 > y0) || V <= 0 || array_width <= 0 || bad_dims(W, H) || z0 < 0 || z1 > V || z0 > z1 ||
       y0 < 0 || y1 > H || y0 > y1)
     return mvs::arg_fail("mvs_proj_inv_rows_d: bad arguments");
-  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1, y0, y1);
+  return mvs::launch_proj_inv(c->stream, V, W, H, array_width, bl_ratio, disp_full, proj, z0, z1, y0, y1,
+                              proj_band != 0);
 }
 
 int mvs_remove_inconsistency_d(mvs_ctx* c, int V, int W, int H, int array_width, float bl_ratio, float fuse,

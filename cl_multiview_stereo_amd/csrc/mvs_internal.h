@@ -109,7 +109,7 @@ int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float
 int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
                   float* proj, float* out, int z0, int z1);
 int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const float* full, float* proj, int z0,
-                    int z1, int ya, int yb);
+                    int z1, int ya, int yb, bool band);
 int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
                          const float* proj, float* out, int z0, int z1, int ya, int yb, bool band);
 

@@ -850,7 +850,7 @@ __device__ __forceinline__ FGrid fgrid(int tiles_x, int y0) {
 // starting maximum (re-gathered once it moves) 4.1 / 4.4 ms, and a
 // row-major grid (every reference of a row in flight together) 6.0 ms.
 __global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full, int V, int W, int H, int aw,
-                                                  float bl, int z0, float* __restrict__ proj, int ya) {
+                                                  float bl, int z0, float* __restrict__ proj, long PO, int ya) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = ya + blockIdx.y, r = z0 + blockIdx.z;
   if (x >= W) return;
   const long P = (long)W * H, p = (long)y * W + x;
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full
       cy++;
     }
   }
-  proj[P * r + p] = md;
+  proj[PO * r + p] = md;  // PO: proj's view stride (W H, or a band's rows x W)
 }
 // The same chain for NC pixels per thread (rows y0 .. y0 + NC - 1 of one
 // column), the NC chains interleaved view by view: per view the NC gathers are
@@ -886,7 +886,8 @@ __global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full
 // not by the TA or L2: ~0.9 us per gather at full occupancy).
 template <int NC>
 __global__ __launch_bounds__(256) void k_proj_inv_mc(const float* __restrict__ full, int V, int W, int H, int aw,
-                                                     float bl, int z0, float* __restrict__ proj, int ya, int yb) {
+                                                     float bl, int z0, float* __restrict__ proj, long PO, int ya,
+                                                     int yb) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y0 = ya + blockIdx.y * NC, r = z0 + blockIdx.z;
   if (x >= W) return;
   const long P = (long)W * H;
@@ -915,7 +916,7 @@ __global__ __launch_bounds__(256) void k_proj_inv_mc(const float* __restrict__ f
   }
 #pragma unroll
   for (int c = 0; c < NC; c++)
-    if (y0 + c < yb) proj[P * r + (long)(y0 + c) * W + x] = md[c];
+    if (y0 + c < yb) proj[PO * r + (long)(y0 + c) * W + x] = md[c];
 }
 
 __global__ void k_remove_incons(const float* __restrict__ proj, const float* __restrict__ full, int V, int W, int H,
@@ -1660,24 +1661,27 @@ int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float
 
 // project_to_reference_inv for reference views [z0, z1): proj slices z0..z1-1
 int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const float* full, float* proj, int z0,
-                    int z1, int ya, int yb) {
+                    int z1, int ya, int yb, bool band) {
   const int NR = yb - ya;  // rows [ya, yb) (the caller checks 0 <= ya <= yb <= H)
   if (z1 <= z0 || NR <= 0) return 0;
+  // band: proj holds rows [ya, yb) only, [V][yb - ya][W] (as launch_remove_incons)
+  const long PO = band ? (long)NR * W : (long)W * H;
+  if (band) proj -= (long)ya * W;
   // MVS_PROJ_NC (read per call): pixels (rows) per thread, 1 = k_proj_inv
   const char* nce = getenv("MVS_PROJ_NC");
   const int nc = nce ? atoi(nce) : 1;
   if (nc == 2)
     hipLaunchKernelGGL(k_proj_inv_mc<2>, dim3((W + 255) / 256, (NR + 1) / 2, z1 - z0), dim3(256), 0, s, full, V, W, H,
-                       aw, bl, z0, proj, ya, yb);
+                       aw, bl, z0, proj, PO, ya, yb);
   else if (nc == 4)
     hipLaunchKernelGGL(k_proj_inv_mc<4>, dim3((W + 255) / 256, (NR + 3) / 4, z1 - z0), dim3(256), 0, s, full, V, W, H,
-                       aw, bl, z0, proj, ya, yb);
+                       aw, bl, z0, proj, PO, ya, yb);
   else if (nc == 8)
     hipLaunchKernelGGL(k_proj_inv_mc<8>, dim3((W + 255) / 256, (NR + 7) / 8, z1 - z0), dim3(256), 0, s, full, V, W, H,
-                       aw, bl, z0, proj, ya, yb);
+                       aw, bl, z0, proj, PO, ya, yb);
   else
     hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, NR, z1 - z0), dim3(256), 0, s, full, V, W, H, aw, bl, z0,
-                       proj, ya);
+                       proj, PO, ya);
   MVS_LAUNCH_CHECK("k_proj_inv");
   return 0;
 }
@@ -1807,7 +1811,7 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
 // pinned order: every projection, then the removal
 int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
                   float* proj, float* out, int z0, int z1) {
-  int rc = launch_proj_inv(s, V, W, H, aw, bl, full, proj, 0, V, 0, H);
+  int rc = launch_proj_inv(s, V, W, H, aw, bl, full, proj, 0, V, 0, H, false);
   if (rc) return rc;
   return launch_remove_incons(s, V, W, H, aw, bl, fuse, full, proj, out, z0, z1, 0, H, false);
 }

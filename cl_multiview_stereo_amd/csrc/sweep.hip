@@ -101,7 +101,7 @@ struct SweepArgs {
 // 128 (measured at C4, 8x4 array, 5 nearest neighbours, all 32 views:
 // TCC_MISS 271 M per launch against 175 M hits, 4.66 ms).  labT (optional)
 // holds such neighbour views re-laid so that consecutive levels' taps are
-// consecutive elements: slot tslot[4 * view + kind] (stride tstride elements)
+// consecutive elements: at labT + tslot[4 * view + kind] * tstride
 // of kind 1 (same camera column: transposed, element (x, y) at x H + y),
 // 2 (dx == dy: sheared, at (x - y + H - 1) H + y) or 3 (dx == -dy: at
 // (x + y) H + y).  With bl != 1 the diagonal shifts drift apart by a row
@@ -785,30 +785,41 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
   // the vertical and diagonal neighbours of the references, re-laid into the
   // context scratch; MVS_SWEEP_TRANSPOSE (read per call) = 0: row-major
   // gathers only, 1: vertical neighbours only, 2 (default): both (A/B)
+  // Slot offsets are in units of H elements (tstride = H): a transposed slot
+  // takes W units, a sheared one W + H - 1.  If the scratch cannot be had, the
+  // row-major kernel runs instead (same results, slower gathers).
   const float4* labT = nullptr;
   const int* tslot = nullptr;
-  const long tstride = (long)(W + H - 1) * H;  // elements per re-laid slot (the sheared layouts' size)
+  const long tstride = H;
   const char* te = getenv("MVS_SWEEP_TRANSPOSE");
   const int tmode = te ? atoi(te) : 2;
   if (tmode > 0) {
     std::vector<int32_t> slot(4 * (size_t)V, -1);
-    int nt = 0;
+    long units = 0;
     for (int z = z0; z < z1; z++)
       for (int k = 0; k < ctx->h_sn[z]; k++) {
         const int v = ctx->h_vs[(size_t)V * z + k];
         if (v < 0 || v >= V) continue;
         const int dx = v % aw - z % aw, dy = v / aw - z / aw;
         const int kind = dx == 0 ? 1 : tmode < 2 ? 0 : dx == dy ? 2 : dx == -dy ? 3 : 0;
-        if (kind && slot[4 * v + kind] < 0) slot[4 * v + kind] = nt++;
+        if (kind && slot[4 * v + kind] < 0 && units + W + H <= INT32_MAX) {
+          slot[4 * v + kind] = (int32_t)units;
+          units += kind == 1 ? W : W + H - 1;
+        }
       }
-    if (nt > 0) {
+    if (units > 0) {
       int rc = 0;
-      float4* buf = (float4*)scratch(ctx, (size_t)nt * tstride * sizeof(float4), &rc);
-      if (rc) return rc;
-      tslot = plan_upload(ctx, slot, &rc);
+      float4* buf = (float4*)scratch(ctx, (size_t)units * tstride * sizeof(float4), &rc);
+      if (rc == MVS_E_NOMEM) {
+        (void)hipGetLastError();  // the failed hipMalloc must not fail the next launch check
+        units = 0;
+      } else if (rc) {
+        return rc;
+      }
+      if (units > 0) tslot = plan_upload(ctx, slot, &rc);
       if (rc) return rc;
       const dim3 tg((W + 31) / 32, (H + 31) / 32);
-      for (int v = 0; v < V; v++)
+      for (int v = 0; v < V && units > 0; v++)
         for (int kind = 1; kind < 4; kind++) {
           const int sl = slot[4 * v + kind];
           if (sl < 0) continue;
@@ -821,7 +832,7 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
             hipLaunchKernelGGL(k_relayout_lab<3>, tg, dim3(256), 0, s, (const float4*)lab, W, H, v, o);
         }
       MVS_LAUNCH_CHECK("k_relayout_lab");
-      labT = buf;
+      if (units > 0) labT = buf;
     }
   }
   auto kern = labT ? (half ? k_sweep_spixl<32, true> : k_sweep_spixl<64, true>)

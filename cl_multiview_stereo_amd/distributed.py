@@ -249,11 +249,10 @@ class ShardedPipeline:
             g(proj[z0:z1], proj)
             return b.remove_inconsistency(full, proj, aw, bl, fuse, z0, z1, out=res)[z0:z1]
         edges = [(H * i // nb, H * (i + 1) // nb) for i in range(nb)]
-        proj, bands = None, []
-        for ya, yb in edges:
-            proj = b.proj_inv(full, aw, bl, z0, z1, proj=proj, rows=(ya, yb))
+        bands = []
+        for ya, yb in edges:  # the block's rows are projected straight into the band's gather buffer
             buf = full.new_empty((V, yb - ya, W))
-            buf[z0:z1] = proj[z0:z1, ya:yb]
+            b.proj_inv(full, aw, bl, z0, z1, proj=buf, rows=(ya, yb), band=True)
             bands.append((ya, yb, buf, g.start(buf[z0:z1], buf)))
         for ya, yb, buf, pending in bands:  # the removal reads each gathered band in place
             res = b.remove_inconsistency(full, pending.wait(), aw, bl, fuse, z0, z1, out=res, rows=(ya, yb), band=True)
@@ -335,8 +334,8 @@ class EngineBackend:
     def spixl_to_image(self, spixl, labels, state, S):
         return self.e.spixl_to_image(spixl.contiguous(), labels.contiguous(), state.contiguous(), S)
 
-    def proj_inv(self, disp_full, aw, bl, z0, z1, proj=None, rows=None):
-        return self.e.proj_inv(disp_full, aw, bl, z0, z1, proj=proj, rows=rows)
+    def proj_inv(self, disp_full, aw, bl, z0, z1, proj=None, rows=None, band=False):
+        return self.e.proj_inv(disp_full, aw, bl, z0, z1, proj=proj, rows=rows, band=band)
 
     def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1, out=None, rows=None, band=False):
         return self.e.remove_inconsistency(disp_full, proj, aw, bl, fuse, z0, z1, out=out, rows=rows, band=band)

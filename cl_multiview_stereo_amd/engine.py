@@ -353,10 +353,15 @@ class Engine:
                                        _ptr(disp_full), _ptr(proj), _ptr(out), int(z0), int(z1)), "mvs_filter_d")
         return proj, out
 
-    def proj_inv(self, disp_full, array_width: int, bl_ratio: float, z0: int, z1: int, proj=None, rows=None):
+    def proj_inv(self, disp_full, array_width: int, bl_ratio: float, z0: int, z1: int, proj=None, rows=None,
+                 band=False):
         """project_to_reference_inv for references [z0, z1) into proj[z0:z1] ([V, H, W]);
-        rows=(y0, y1): image rows [y0, y1) only."""
+        rows=(y0, y1): image rows [y0, y1) only -- with band=True `proj` is that row
+        band alone, [V, y1 - y0, W] (the buffer its all-gather fills)."""
         V, H, W = disp_full.shape
+        if band:
+            if rows is None or proj is None or tuple(proj.shape) != (V, rows[1] - rows[0], W):
+                raise ValueError("band=True needs rows=(y0, y1) and proj of shape [V, y1 - y0, W]")
         proj = self.empty((V, H, W), torch.float32) if proj is None else proj
         self._stream()
         if rows is None:
@@ -364,8 +369,8 @@ class Engine:
                                              _ptr(disp_full), _ptr(proj), int(z0), int(z1)), "mvs_proj_inv_d")
         else:
             _lib.check(self.L.mvs_proj_inv_rows_d(self.ctx, V, W, H, int(array_width), C.c_float(bl_ratio),
-                                                  _ptr(disp_full), _ptr(proj), int(z0), int(z1), int(rows[0]),
-                                                  int(rows[1])), "mvs_proj_inv_rows_d")
+                                                  _ptr(disp_full), _ptr(proj), int(bool(band)), int(z0), int(z1),
+                                                  int(rows[0]), int(rows[1])), "mvs_proj_inv_rows_d")
         return proj
 
     def remove_inconsistency(self, disp_full, proj, array_width: int, bl_ratio: float, fuse: float, z0: int, z1: int,

@@ -227,9 +227,11 @@ int mvs_remove_inconsistency_d(mvs_ctx* ctx, int V, int W, int H, int array_widt
  * band's removal can start once that band's proj rows have arrived.  The
  * disparity stack is read in full by both (reprojected gathers).  proj_band
  * 0: proj is the full [V][H][W] stack; 1: proj is the band alone,
- * [V][y1 - y0][W] (what a row band's all-gather delivers). */
+ * [V][y1 - y0][W] (what a row band's all-gather delivers; the projection
+ * writes its block's rows straight into the band buffer).  ABI 0.4: proj_band
+ * added to mvs_proj_inv_rows_d. */
 int mvs_proj_inv_rows_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, const float* disp_full,
-                        float* proj, int z0, int z1, int y0, int y1);
+                        float* proj, int proj_band, int z0, int z1, int y0, int y1);
 int mvs_remove_inconsistency_rows_d(mvs_ctx* ctx, int V, int W, int H, int array_width, float bl_ratio, float fuse,
                                     const float* disp_full, const float* proj, int proj_band, float* out, int z0,
                                     int z1, int y0, int y1);

@@ -79,11 +79,14 @@ class OracleBackend:
     def spixl_to_image(self, spixl, labels, state, S):
         return torch.from_numpy(orc.spixl_to_image(_np(spixl), _np(labels).view(np.uint32), _np(state), S))
 
-    def proj_inv(self, disp_full, aw, bl, z0, z1, proj=None, rows=None):
+    def proj_inv(self, disp_full, aw, bl, z0, z1, proj=None, rows=None, band=False):
         oproj, _ = orc.filt(_np(disp_full), aw, bl, 1.0)
         out = torch.full(oproj.shape, float("nan")) if proj is None else proj
         ya, yb = rows if rows is not None else (0, oproj.shape[1])
-        out[z0:z1, ya:yb] = torch.from_numpy(oproj[z0:z1, ya:yb])
+        if band:  # proj is the row band alone, [V, yb - ya, W]
+            out[z0:z1] = torch.from_numpy(oproj[z0:z1, ya:yb])
+        else:
+            out[z0:z1, ya:yb] = torch.from_numpy(oproj[z0:z1, ya:yb])
         return out
 
     def remove_inconsistency(self, disp_full, proj, aw, bl, fuse, z0, z1, out=None, rows=None, band=False):

@@ -366,6 +366,11 @@ def test_filter_row_bands(engine, monkeypatch, aw, ah, kern):
         for ya, yb in bands:
             engine.proj_inv(d, aw, 1.0359, 0, V, proj=proj, rows=(ya, yb))
         assert_bits(proj.cpu().numpy(), oproj, f"banded projection (NC {nc})")
+        for z0, z1 in ((0, V // 3), (V // 3, V)):  # straight into band buffers, [V, yb - ya, W]
+            for ya, yb in bands:
+                buf = torch.full((V, yb - ya, W), float("nan"), device=d.device)
+                engine.proj_inv(d, aw, 1.0359, z0, z1, proj=buf, rows=(ya, yb), band=True)
+                assert_bits(buf[z0:z1].cpu().numpy(), oproj[z0:z1, ya:yb], f"band-buffer projection (NC {nc})")
     for band in (False, True):  # proj rows within the full stack / the band alone, [V, yb - ya, W]
         out = torch.full((V, H, W), -1.0, device=d.device)
         for z0, z1 in ((0, V // 3), (V // 3, V)):

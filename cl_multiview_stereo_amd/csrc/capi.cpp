@@ -299,9 +299,11 @@ int mvs_box_stats_range_d(mvs_ctx* c, const uint8_t* l8, int V, int W, int H, in
 int mvs_set_ncc_variant(mvs_ctx* c, int waves, int levels_per_wave, int band_w, int general_rows) {
   if (!c) return mvs::arg_fail("null context");
   if ((waves != 0 && waves != 4 && waves != 8) || (levels_per_wave != 0 && levels_per_wave != 1 &&
-      levels_per_wave != 2 && levels_per_wave != 4) || (band_w != 0 && band_w != 128 && band_w != 192 &&
-      band_w != 256) || (waves == 8 && levels_per_wave != 0 && levels_per_wave != 4))
-    return mvs::arg_fail("mvs_set_ncc_variant: waves 0|4|8, levels_per_wave 0|1|2|4 (8 waves: 4), band_w 0|128|192|256");
+      levels_per_wave != 2 && levels_per_wave != 4) ||
+      (band_w != 0 && band_w != 64 && band_w != 80 && band_w != 96 && band_w != 128 && band_w != 192 &&
+       band_w != 256))
+    return mvs::arg_fail(
+        "mvs_set_ncc_variant: waves 0|4|8, levels_per_wave 0|1|2|4, band_w 0|64|80|96|128|192|256");
   c->ncc_nw = waves;
   c->ncc_dpw = levels_per_wave;
   c->ncc_bw = band_w;

@@ -334,22 +334,28 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // is image column x0 - txmax + j; band pair row i of pk holds image rows
   // 2(pm0+i), 2(pm0+i)+1 with pm0 = (y0-R-tymax)>>1 (stats: (y0-tymax)>>1).
   // Columns and pairs are clamped into the image: edge pixels' windows are
-  // invalid (NaN ivr) for R >= 2, so clamped cells never contribute.
+  // invalid (NaN ivr) for R >= 2, so clamped cells never contribute.  A pair
+  // row takes 64 + span columns (span: this neighbour's column-shift range
+  // over the chunk) in 64-column DMA pieces at columns 0, 64, ..., the last
+  // one moved back to end at column 64 + span: it never writes past the row,
+  // so the row pitch BW need only hold 64 + the widest span (not a multiple
+  // of 64), and the overlapped columns get the same bytes twice.
   auto stage = [&](int t, int n, int b) {
     const NccRec& e = rec[NW * t];
-    const int bhp = e.bhp, shp = e.shp & 0xffff, nblk = e.shp >> 16;
+    const int bhp = e.bhp, shp = e.shp & 0xffff, span = e.shp >> 16, nblk = (span + 127) >> 6;
     const int pm0 = (y0 - R - e.tymax) >> 1, sm0 = (y0 - e.tymax) >> 1;
     const long vo = (long)a.view[ref][n] * Pv;
     u32x4* npk = nbase + b * nbuf;
     u32x4* nst = npk + a.pk_pairs * BW;
     for (int cb = 0; cb < nblk; cb++) {
-      const int xx = min(max(x0 - e.txmax + cb * 64 + lane, 0), W - 1);
+      const int c0 = min(cb * 64, span);
+      const int xx = min(max(x0 - e.txmax + c0 + lane, 0), W - 1);
       const uint2* gpk = pk + vo + 2 * xx;
       const uint2* gst = stats + vo + 2 * xx;
       for (int i = wave; i < bhp; i += NW)
-        glds_b128(gpk + 2L * W * min(max(pm0 + i, 0), Hp2 - 1), npk + i * BW + cb * 64);
+        glds_b128(gpk + 2L * W * min(max(pm0 + i, 0), Hp2 - 1), npk + i * BW + c0);
       for (int i = wave; i < shp; i += NW)
-        glds_b128(gst + 2L * W * min(max(sm0 + i, 0), Hp2 - 1), nst + i * BW + cb * 64);
+        glds_b128(gst + 2L * W * min(max(sm0 + i, 0), Hp2 - 1), nst + i * BW + c0);
     }
   };
   float E[DPW][TH];
@@ -617,13 +623,12 @@ NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const fl
       const int pr = pb - 2 * floor_half(pb), sr = sb - 2 * floor_half(sb);  // its parity in the pair band
       const int bhp = (pr + NR + tymax - tymin + 1) >> 1;  // pairs covering every level's rows
       const int shp = (sr + TH + tymax - tymin + 1) >> 1;
-      const int nblk = (64 + txmax - txmin + 63) >> 6;
       for (int w = 0; w < NW; w++) {
         int32_t* e = p.table.data() + (((size_t)c * nn + n) * NW + w) * RW;
         e[0] = txmax;
         e[1] = tymax;
         e[2] = bhp;
-        e[3] = shp | (nblk << 16);
+        e[3] = shp | ((txmax - txmin) << 16);  // stage(): pieces of 64 columns covering 64 + span
         for (int j = 0; j < DPW; j++) {
           const int dl = c * DC + w + NW * j;
           if (dl >= D) {  // dummy level past the end: the band origin's even rows
@@ -641,7 +646,7 @@ NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const fl
       p.pk_pairs = std::max(p.pk_pairs, bhp);
       p.st_pairs = std::max(p.st_pairs, shp);
     }
-  p.band_w = (64 + spx + 63) & ~63;  // whole 64-column LDS-DMA pieces per pair row
+  p.band_w = 64 + spx;  // columns per pair row (stage() never writes past them)
   return p;
 }
 
@@ -678,10 +683,12 @@ template <int K, int DPW, int NW>
 bool try_plan(const mvs_ctx* ctx, const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl,
               size_t cap, NccChoice& o) {
   NccPlan p = make_plan<K, 8, DPW, NW>(levels, D, nn, fdx, fdy, bl);
-  // the band's pair-row stride is the template BW: the smallest of 128 / 192 /
-  // 256 holding band_w, or a wider one forced through mvs_set_ncc_variant
-  const int bw = std::max(std::max(p.band_w, ctx->ncc_bw), 128);
-  const int bwt = bw <= 128 ? 128 : bw <= 192 ? 192 : 256;
+  // the band's pair-row stride is the template BW: the smallest of 64 / 80 /
+  // 96 / 128 / 192 / 256 holding band_w, or a wider one forced through
+  // mvs_set_ncc_variant.  A vertical-only list needs 64, a diagonal or
+  // horizontal neighbour 64 + the chunk's shift range (C4: 71 / 79 / 95)
+  const int bw = std::max(p.band_w, ctx->ncc_bw);
+  const int bwt = bw <= 64 ? 64 : bw <= 80 ? 80 : bw <= 96 ? 96 : bw <= 128 ? 128 : bw <= 192 ? 192 : 256;
   const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * bwt;
   if (lds > cap || bw > 256) return false;
   o.dpw = DPW;
@@ -716,6 +723,10 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
     const size_t cap = (size_t)160 * 1024;
     if (nw_pref >= 8 && dpw_pref >= 4) {
       MVS_NCC_TRY(4, 8)
+    } else if (nw_pref >= 8 && dpw_pref >= 2) {
+      MVS_NCC_TRY(2, 8)
+    } else if (nw_pref >= 8) {
+      MVS_NCC_TRY(1, 8)
     } else if (dpw_pref >= 4) {
       MVS_NCC_TRY(4, 4)
     } else if (dpw_pref >= 2) {
@@ -726,6 +737,7 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
   }
   for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
     if (nw_pref >= 8 && dpw_pref >= 4) MVS_NCC_TRY(4, 8)
+    if (nw_pref >= 8 && dpw_pref >= 2) MVS_NCC_TRY(2, 8)
     if (dpw_pref >= 4) MVS_NCC_TRY(4, 4)
     if (dpw_pref >= 2) MVS_NCC_TRY(2, 4)
     MVS_NCC_TRY(1, 4)
@@ -738,10 +750,16 @@ template <int K, int DPW, int NW>
 int launch_bw_even(mvs_ctx* ctx, int bwt, bool even, const uint2* stats, const uint2* pk, const NccRec* plan,
                    NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
   if (even && !ctx->ncc_general) {
+    if (bwt == 64) return launch_ncc_bw<K, 8, DPW, NW, 64, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+    if (bwt == 80) return launch_ncc_bw<K, 8, DPW, NW, 80, true>(ctx, stats, pk, plan, a, vol, wo, lds);
+    if (bwt == 96) return launch_ncc_bw<K, 8, DPW, NW, 96, true>(ctx, stats, pk, plan, a, vol, wo, lds);
     if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, true>(ctx, stats, pk, plan, a, vol, wo, lds);
     if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, true>(ctx, stats, pk, plan, a, vol, wo, lds);
     return launch_ncc_bw<K, 8, DPW, NW, 256, true>(ctx, stats, pk, plan, a, vol, wo, lds);
   }
+  if (bwt == 64) return launch_ncc_bw<K, 8, DPW, NW, 64, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 80) return launch_ncc_bw<K, 8, DPW, NW, 80, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 96) return launch_ncc_bw<K, 8, DPW, NW, 96, false>(ctx, stats, pk, plan, a, vol, wo, lds);
   if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, false>(ctx, stats, pk, plan, a, vol, wo, lds);
   if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, false>(ctx, stats, pk, plan, a, vol, wo, lds);
   return launch_ncc_bw<K, 8, DPW, NW, 256, false>(ctx, stats, pk, plan, a, vol, wo, lds);
@@ -750,6 +768,8 @@ template <int K>
 int launch_variant(mvs_ctx* ctx, const NccChoice& c, int bwt, bool even, const uint2* stats, const uint2* pk,
                    const NccRec* plan, NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
   if (c.dpw == 4 && c.nw == 8) return launch_bw_even<K, 4, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 2 && c.nw == 8) return launch_bw_even<K, 2, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 1 && c.nw == 8) return launch_bw_even<K, 1, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
   if (c.dpw == 4) return launch_bw_even<K, 4, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
   if (c.dpw == 2) return launch_bw_even<K, 2, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
   return launch_bw_even<K, 1, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);

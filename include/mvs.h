@@ -177,8 +177,8 @@ int mvs_ncc_wta_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* 
 int mvs_ncc_wta_range_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a,
                         int K, int z0, int z1, float* disp, float* conf);
 /* Tuning / test hook: the NCC sweep variant this context tries first (0 =
- * automatic): waves per workgroup 4|8, levels per wave 1|2|4 (8 waves: 4),
- * minimum LDS band width 128|192|256 columns, general_rows 1 = the kernel
+ * automatic): waves per workgroup 4|8, levels per wave 1|2|4,
+ * minimum LDS band width 64|80|96|128|192|256 columns, general_rows 1 = the kernel
  * that handles band rows starting on either row parity even when all start
  * on a pair.  Variants that do not fit the LDS fall back as in the default
  * chain.  mvs_ncc_last_variant reports the last launch as

@@ -144,46 +144,59 @@ def test_c4_geometry(eng, bl):
     assert dpws & {1, 2}, f"C4 geometry should need a narrower variant, saw {sorted(variants)}"
 
 
-_VARIANTS = [(8, 4), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation of the chain
+_VARIANTS = [(8, 4), (8, 2), (8, 1), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation
+_BANDS = (64, 80, 96, 128, 192, 256)  # band pitch templates (columns per pair row)
 
 
 @pytest.mark.parametrize("K", [5, 7])
-@pytest.mark.parametrize("geom", ["horizontal", "vertical"])
+@pytest.mark.parametrize("geom", ["horizontal", "vertical", "vertical_only"])
 def test_every_ncc_variant(eng, K, geom):
     """Force each (waves, levels per wave) x band width x row-parity variant,
     plain and fused, and compare with the oracle; the launch must report the
-    forced variant."""
+    forced variant (a band width below what the shifts need rises to the
+    smallest pitch that holds them: 128 horizontal, 80 for one column of
+    shift range, 64 for vertical neighbours only)."""
     if geom == "horizontal":  # every band row starts on a pair: the EVEN kernel is eligible
         aw, ah, nh, nv, bl, W, H, dmax = 4, 1, 2, 0, 1.0, 150, 40, 39
-    else:  # vertical neighbours with fractional shifts: odd band-row starts.  Few levels, so
-        # that even the 32-level chunk's band at 256 columns fits the 160 KB LDS
+    elif geom == "vertical":  # vertical neighbours with fractional shifts: odd band-row starts.  Few
+        # levels, so that even the 32-level chunk's band at 256 columns fits the 160 KB LDS
         aw, ah, nh, nv, bl, W, H, dmax = 2, 3, 1, 1, 1.0359, 120, 56, 4
+    else:  # a 1 x 3 column of cameras: no column shift at all
+        aw, ah, nh, nv, bl, W, H, dmax = 1, 3, 0, 1, 1.0359, 100, 56, 4
     stack, _ = synth.make_stack(W, H, aw, ah, 0, dmax, bl, 77 + K)
     cam = _array(aw, ah, 0, dmax, nh=nh, nv=nv, bl=bl)
     lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
     l8h = l8.cpu().numpy()
     box = eng.box_stats(l8, K)
-    z = 1 if geom == "horizontal" else 3
+    z = 1
     want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, bl, K, z)
     od, oc = orc.wta(want, cam.levels)
-    evens = set()
+    evens, seen = set(), set()
+    dxs = [int(v) % aw - z % aw for v in cam.view_subset[z, :int(cam.subset_num[z])]]
     for nw, dpw in _VARIANTS:
-        for bw in (128, 192, 256):
+        dc = nw * dpw  # columns of shift range in a chunk of dc whole levels: |dx| (dc' - 1)
+        need = 64 + max(abs(dx) for dx in dxs) * (min(dc, dmax + 1) - 1)
+        need = min(b for b in _BANDS if b >= need)
+        for bw in _BANDS:
             for general in (False, True):
                 eng.set_ncc_variant(nw, dpw, bw, general)
                 tag = f"K{K} nw{nw} dpw{dpw} bw{bw} general{int(general)}"
                 vol = eng.ncc_volume(l8, box, cam, z, K)
                 v = eng.ncc_last_variant()
-                assert (v["K"], v["NW"], v["DPW"], v["BW"], v["FUSE"]) == (K, nw, dpw, bw, 0), (tag, v)
+                assert (v["K"], v["NW"], v["DPW"], v["FUSE"]) == (K, nw, dpw, 0), (tag, v)
+                assert v["BW"] == max(bw, need), (tag, v)
+                seen.add(v["BW"])
                 if general:
                     assert v["EVEN"] == 0, (tag, v)
                 evens.add(v["EVEN"])
                 same(vol, want, f"volume {tag}")
                 fd, fc = eng.ncc_wta(l8, box, cam, z, K)
                 v = eng.ncc_last_variant()
-                assert (v["NW"], v["DPW"], v["BW"], v["FUSE"]) == (nw, dpw, bw, 1), (tag, v)
+                assert (v["NW"], v["DPW"], v["BW"], v["FUSE"]) == (nw, dpw, max(bw, need), 1), (tag, v)
                 same(fd, od, f"fused disp {tag}")
                 same(fc, oc, f"fused conf {tag}")
+    # every pitch from the narrowest the geometry allows (4-level chunks) up
+    assert seen == {b for b in _BANDS if b >= {"horizontal": 80, "vertical": 80, "vertical_only": 64}[geom]}, seen
     # K = 5 horizontal bands start on a row pair (R + tymax even); K = 7 (R = 3)
     # and fractional vertical shifts start on odd rows
     assert evens == ({0, 1} if geom == "horizontal" and K == 5 else {0})

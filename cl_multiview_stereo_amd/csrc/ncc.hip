@@ -479,7 +479,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int y = y0 + o;
     const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
     const int var = NK * s2 - s1 * s1;
-    sr[o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
+    // fused: only wave 0 needs s_r (it publishes it in LDS), so the other
+    // waves skip the correctly rounded sqrt + divide of every row
+    if (!FUSE || wave == 0)
+      sr[o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
     rsn[o >> 1][o & 1] = -(float)s1;
   }
   if (FUSE && wave == 0) {

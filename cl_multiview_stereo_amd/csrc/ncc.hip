@@ -728,8 +728,6 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
       MVS_NCC_TRY(4, 8)
     } else if (nw_pref >= 8 && dpw_pref >= 2) {
       MVS_NCC_TRY(2, 8)
-    } else if (nw_pref >= 8) {
-      MVS_NCC_TRY(1, 8)
     } else if (dpw_pref >= 4) {
       MVS_NCC_TRY(4, 4)
     } else if (dpw_pref >= 2) {
@@ -772,7 +770,6 @@ int launch_variant(mvs_ctx* ctx, const NccChoice& c, int bwt, bool even, const u
                    const NccRec* plan, NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
   if (c.dpw == 4 && c.nw == 8) return launch_bw_even<K, 4, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
   if (c.dpw == 2 && c.nw == 8) return launch_bw_even<K, 2, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
-  if (c.dpw == 1 && c.nw == 8) return launch_bw_even<K, 1, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
   if (c.dpw == 4) return launch_bw_even<K, 4, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
   if (c.dpw == 2) return launch_bw_even<K, 2, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
   return launch_bw_even<K, 1, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);

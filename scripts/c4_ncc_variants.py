@@ -35,7 +35,7 @@ def main():
         "d1": {z: [z + aw + 1]},
         "knn5": {z: params.nearest_neighbours(aw, ah, 5)[z]},
     }
-    variants = [(0, 0), (8, 4), (8, 2), (8, 1), (4, 4), (4, 2), (4, 1)]
+    variants = [(0, 0), (8, 4), (8, 2), (4, 4), (4, 2), (4, 1)]
     res = {}
     for name, nb in cases.items():
         lists = [nb.get(v, []) for v in range(V)]

@@ -144,7 +144,7 @@ def test_c4_geometry(eng, bl):
     assert dpws & {1, 2}, f"C4 geometry should need a narrower variant, saw {sorted(variants)}"
 
 
-_VARIANTS = [(8, 4), (8, 2), (8, 1), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation
+_VARIANTS = [(8, 4), (8, 2), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation
 _BANDS = (64, 80, 96, 128, 192, 256)  # band pitch templates (columns per pair row)
 
 

@@ -31,9 +31,21 @@ exchange exactly what later stages read from other views:
                                                               gathered spixl/labels/state
                                                               (no refinement: all-gather
                                                               the disparity maps)
-  projection (a15 i), own block     all disparity maps        all-gather proj
-  removal (a15 ii), own block       all proj slices, all      -
-                                    disparity maps
+  projection (a15 i), own ROWS of   all disparity maps        none
+  every reference view
+  removal (a15 ii), own rows of     the proj slices at the    rows -> views exchange of
+  every reference view              pixel (same rows), all    the filtered maps (each rank
+                                    disparity maps            receives its views' other
+                                                              rows: 1/world of a gather)
+
+The filter is sharded by image ROWS (filter_shard="rows", the default): every
+rank holds all V disparity maps after the fusion, and the projection and the
+removal at a pixel read only those maps and the proj slices at that pixel, so
+a rank filters rows [y0, y1) of every reference view with no proj all-gather
+(the reference-view form, filter_shard="views", all-gathers the block's proj
+slices in row bands: ~7/8 of V x H x W x 4 bytes into every rank).  The
+world-1-like grid (every reference of a row in flight together) also keeps
+the removal's gathers as local as in the unsharded run.
 
 The backend does the compute for one rank: ``EngineBackend`` (HIP kernels
 through libmvs.so) on a GPU.  The tests substitute a CPU stand-in of the same
@@ -87,6 +99,40 @@ class ViewGather:
     @property
     def block(self) -> tuple[int, int]:
         return self.blocks[self.rank]
+
+    def row_band(self, H: int) -> tuple[int, int]:
+        """This rank's rows [y0, y1) of a row-sharded stage (balanced contiguous)."""
+        return all_blocks(H, self.world)[self.rank]
+
+    def rows_to_views(self, rows_full: torch.Tensor) -> torch.Tensor:
+        """rows_full [V, H, W] holds this rank's row band of every view; returns
+        [z1 - z0, H, W]: every row of this rank's view block.  Rank s sends rank d
+        the rows of d's views in s's band (point to point, batched: RCCL groups
+        them; gloo has no all_to_all)."""
+        V, H = rows_full.shape[:2]
+        z0, z1 = self.block
+        if self.world == 1:
+            return rows_full[z0:z1]
+        bands = all_blocks(H, self.world)
+        ya, yb = bands[self.rank]
+        out = rows_full.new_empty((z1 - z0,) + tuple(rows_full.shape[1:]))
+        out[:, ya:yb] = rows_full[z0:z1, ya:yb]
+        ops, recv = [], []
+        for d in range(self.world):
+            if d == self.rank:
+                continue
+            b0, b1 = self.blocks[d]
+            send = rows_full[b0:b1, ya:yb].contiguous()
+            r0, r1 = bands[d]
+            buf = rows_full.new_empty((z1 - z0, r1 - r0) + tuple(rows_full.shape[2:]))
+            ops.append(dist.P2POp(dist.isend, send, d, group=self.group))
+            ops.append(dist.P2POp(dist.irecv, buf, d, group=self.group))
+            recv.append((r0, r1, buf, send))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for r0, r1, buf, _ in recv:
+            out[:, r0:r1] = buf
+        return out
 
     def start(self, local: torch.Tensor, full: torch.Tensor) -> "PendingGather":
         """The same all-gather, asynchronous: the collective is issued behind the
@@ -179,12 +225,18 @@ class ShardedPipeline:
     EngineBackend for the interface)."""
 
     def __init__(self, backend, settings: params.Settings, cam, gather: ViewGather,
-                 pixel_cost: str | None = "ncc", refine: bool = True, filt: bool = True, proj_bands: int | None = None):
+                 pixel_cost: str | None = "ncc", refine: bool = True, filt: bool = True, proj_bands: int | None = None,
+                 filter_shard: str | None = None):
         self.b, self.st, self.cam, self.g = backend, settings, cam, gather
         self.pixel_cost, self.refine, self.filt = pixel_cost, refine, filt
-        # row bands of the pipelined proj all-gather (1: one gather; default: 2
-        # when there is a gather to hide, i.e. world > 1)
+        # row bands of the pipelined proj all-gather of the reference-view
+        # sharded filter (1: one gather; default: 2 when there is a gather to
+        # hide, i.e. world > 1)
         self.proj_bands = proj_bands if proj_bands is not None else (2 if gather.world > 1 else 1)
+        # "rows" (default; MVS_FILTER_SHARD overrides) or "views"
+        self.filter_shard = filter_shard or os.environ.get("MVS_FILTER_SHARD", "rows")
+        if self.filter_shard not in ("rows", "views"):
+            raise ValueError("filter_shard must be 'rows' or 'views'")
 
     def run(self, rgbx: torch.Tensor) -> ShardOutput:
         st, b, g = self.st, self.b, self.g
@@ -218,7 +270,7 @@ class ShardedPipeline:
         out.spixl = g(spixl[z0:z1], spixl)  # centres + seeds (s7) of every view
         if narrow:
             pending.wait()
-            out.labels = l16.to(torch.int32).bitwise_and_(0xFFFF)
+            out.labels = l16.view(torch.uint16).to(torch.int32)  # one widening pass
         else:
             out.labels = pending.wait()
         spixl, labels = out.spixl, out.labels
@@ -233,6 +285,27 @@ class ShardedPipeline:
         return out
 
     def _filter(self, full, z0, z1):
+        if self.filter_shard == "rows":
+            return self._filter_rows(full)
+        return self._filter_views(full, z0, z1)
+
+    def _filter_rows(self, full):
+        """project_to_reference_inv + remove_view_inconsistency (clcode.cl:1995-2101)
+        for this rank's rows of EVERY reference view: the projection reads only
+        the disparity maps, which every rank holds, and the removal at a pixel
+        reads the proj slices at that pixel, which this rank has just computed.
+        Then each rank receives the other rows of its own views."""
+        st, b, g = self.st, self.b, self.g
+        aw, bl, fuse = st.array_width, st.bl_ratio, st.fuse
+        V, H, W = full.shape
+        ya, yb = g.row_band(H)
+        buf = full.new_empty((V, yb - ya, W))
+        b.proj_inv(full, aw, bl, 0, V, proj=buf, rows=(ya, yb), band=True)
+        res = full.new_empty(full.shape)  # only rows [ya, yb) are written
+        res = b.remove_inconsistency(full, buf, aw, bl, fuse, 0, V, out=res, rows=(ya, yb), band=True)
+        return g.rows_to_views(res)
+
+    def _filter_views(self, full, z0, z1):
         """project_to_reference_inv for the block, then every rank holds all proj
         slices, which remove_view_inconsistency reads (clcode.cl:2054).  The
         removal at a pixel reads the proj slices at that pixel only, so with

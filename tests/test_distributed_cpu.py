@@ -54,7 +54,7 @@ def _unsharded(c, b):
     return dict(spixl=sp, labels=lb, refined=ref["disp"], filt=filt, disp=disp)
 
 
-def _worker(rank, world, port, name, outdir, bands=None):
+def _worker(rank, world, port, name, outdir, bands=None, shard=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -68,7 +68,8 @@ def _worker(rank, world, port, name, outdir, bands=None):
         st = _settings(c)
         cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
         g = ViewGather(b["V"])
-        pipe = ShardedPipeline(OracleBackend(), st, cam, g, pixel_cost="ncc", refine=True, filt=True, proj_bands=bands)
+        pipe = ShardedPipeline(OracleBackend(), st, cam, g, pixel_cost="ncc", refine=True, filt=True, proj_bands=bands,
+                               filter_shard=shard)
         out = pipe.run(torch.from_numpy(b["stack"]))
         np.savez(os.path.join(outdir, f"r{rank}.npz"), z=np.array([out.z0, out.z1]), spixl=out.spixl.numpy(),
                  labels=out.labels.numpy().view(np.uint32), disp=out.disp.numpy(),
@@ -77,14 +78,17 @@ def _worker(rank, world, port, name, outdir, bands=None):
         dist.destroy_process_group()
 
 
-# bands: row bands of the pipelined proj all-gather (None: the default, 2 at world > 1)
-@pytest.mark.parametrize("name,world,bands", [("c3x1_s8", 2, None), ("c3x1_s8", 3, None), ("c2x2_s12", 2, 1),
-                                              ("c3x1_s8", 1, None), ("c3x1_s8", 1, 3)])
-def test_sharded_equals_unsharded(name, world, bands):
+# shard: the filter's sharding ("rows", the default, or "views"); bands: row
+# bands of the "views" form's pipelined proj all-gather (None: 2 at world > 1)
+@pytest.mark.parametrize("name,world,bands,shard", [("c3x1_s8", 2, None, "rows"), ("c3x1_s8", 3, None, "rows"),
+                                                    ("c2x2_s12", 2, None, "rows"), ("c3x1_s8", 2, None, "views"),
+                                                    ("c3x1_s8", 3, None, "views"), ("c2x2_s12", 2, 1, "views"),
+                                                    ("c3x1_s8", 1, None, "rows"), ("c3x1_s8", 1, 3, "views")])
+def test_sharded_equals_unsharded(name, world, bands, shard):
     c, b = _case(name)
     want = _unsharded(c, b)
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), name, d, bands), nprocs=world, join=True,
+        mp.start_processes(_worker, args=(world, _free_port(), name, d, bands, shard), nprocs=world, join=True,
                            start_method="spawn")
         seen = []
         for r in range(world):
@@ -153,10 +157,10 @@ def test_async_gather_gloo():
 
 def test_labels_16bit_round_trip():
     """The 16-bit labels gather (distributed._narrow_labels): int32 -> int16
-    (wrap) -> bytes -> int16 -> int32 & 0xFFFF is the identity on 0..65535."""
+    (wrap) -> bytes -> int16 -> uint16 -> int32 is the identity on 0..65535."""
     from cl_multiview_stereo_amd.distributed import _bytes
     t = torch.arange(0, 1 << 16, dtype=torch.int32).view(4, 128, 128)
     l16 = t.to(torch.int16)
     b = _bytes(l16).clone()
-    back = b.view(torch.int16).view(4, 128, 128).to(torch.int32).bitwise_and_(0xFFFF)
+    back = b.view(torch.int16).view(4, 128, 128).view(torch.uint16).to(torch.int32)
     assert torch.equal(back, t)

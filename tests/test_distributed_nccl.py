@@ -4,7 +4,8 @@ sharded run must give the unsharded oracle's depth maps bit for bit -- the
 same bar as tests/test_distributed_cpu.py (gloo + oracle stand-in), here with
 the product compute and the overlapped collectives on real streams: the async
 in-place labels all-gather (16-bit) still in flight during the sweeps, and the
-row-banded proj all-gather pipelined with the cross-view filter.
+row-sharded cross-view filter's point-to-point rows -> views exchange (and the
+reference-view form's row-banded proj all-gather).
 
 Skipped with fewer than 2 GPUs visible (the round's 1-GPU boxes); the
 driver's multi-GPU node runs it."""
@@ -25,7 +26,7 @@ pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs (RCCL world 2)")]
 
 
-def _worker(rank, world, port, name, outdir, bands):
+def _worker(rank, world, port, name, outdir, bands, shard):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
@@ -38,7 +39,7 @@ def _worker(rank, world, port, name, outdir, bands):
         e = Engine(rank)
         cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
         pipe = ShardedPipeline(EngineBackend(e, fused=True), _settings(c), cam, ViewGather(b["V"]), pixel_cost="ncc",
-                               refine=True, filt=True, proj_bands=bands)
+                               refine=True, filt=True, proj_bands=bands, filter_shard=shard)
         out = pipe.run(torch.from_numpy(b["stack"]).cuda())
         torch.cuda.synchronize()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), z=np.array([out.z0, out.z1]), spixl=out.spixl.cpu().numpy(),
@@ -48,12 +49,13 @@ def _worker(rank, world, port, name, outdir, bands):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,bands", [("c3x1_s8", None), ("c2x2_s12", 1)])
-def test_sharded_rccl_equals_unsharded(name, bands):
+@pytest.mark.parametrize("name,bands,shard", [("c3x1_s8", None, "rows"), ("c2x2_s12", None, "views"),
+                                              ("c2x2_s12", 1, "views")])
+def test_sharded_rccl_equals_unsharded(name, bands, shard):
     c, b = _case(name)
     want = _unsharded(c, b)
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(2, _free_port(), name, d, bands), nprocs=2, join=True,
+        mp.start_processes(_worker, args=(2, _free_port(), name, d, bands, shard), nprocs=2, join=True,
                            start_method="spawn")
         for r in range(2):
             with np.load(os.path.join(d, f"r{r}.npz")) as z:

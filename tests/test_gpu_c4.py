@@ -85,7 +85,11 @@ def test_c4_world1_matches_oracle(engine):
 
 
 @pytest.mark.gpu
-def test_c4_world8_replay_matches_oracle(engine):
+@pytest.mark.parametrize("shard", ["rows", "views"])
+def test_c4_world8_replay_matches_oracle(engine, shard):
+    """shard: the filter sharded by image rows (the default: every reference
+    view's rows of the rank's band, then the rows -> views exchange) or by
+    reference view (row-banded proj all-gather)."""
     stack, levels, vs, sn, st = _case()
     want = _oracle()
     V = AW * AH
@@ -93,10 +97,11 @@ def test_c4_world8_replay_matches_oracle(engine):
     be = EngineBackend(engine, fused=True)
     rgbx = torch.from_numpy(stack).cuda()
     rg = RecordingGather(V)
-    ShardedPipeline(be, st, cam, rg, pixel_cost="ncc", refine=True, filt=True, proj_bands=2).run(rgbx)
+    kw = dict(pixel_cost="ncc", refine=True, filt=True, proj_bands=2, filter_shard=shard)
+    ShardedPipeline(be, st, cam, rg, **kw).run(rgbx)
     for r in range(8):
         g = ReplayGather(V, r, 8, list(rg.rec))
-        out = ShardedPipeline(be, st, cam, g, pixel_cost="ncc", refine=True, filt=True, proj_bands=2).run(rgbx)
+        out = ShardedPipeline(be, st, cam, g, **kw).run(rgbx)
         z0, z1 = g.block
         assert (z0, z1) == (4 * r, 4 * r + 4)
         _check(out, want, z0, z1)

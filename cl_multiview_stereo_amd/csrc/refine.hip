@@ -1368,11 +1368,32 @@ __device__ __forceinline__ void ri_prep(RiShared& S, const float* __restrict__ p
   S.nd[lane] = nd;
 }
 
+// An upper bound on #{k in [k0, k1] : 0 <= p - round(fl(dd * k)) <= lim - 1},
+// the camera columns (rows) whose reprojection of pixel coordinate p lands in
+// the image.  round(v) in [p - lim + 1, p] needs v in [p - lim + 0.5, p + 0.5],
+// and round(fl(dd * k)) is monotone in k, so the valid k are one interval;
+// its ends come from one reciprocal with a 1e-3 margin (dd * k is within
+// 2^-23 of the product, and only |k| <= 8 matters), so the count can only
+// come out high.  dd != 0 (candidates are nonzero).
+__device__ __forceinline__ int in_span_ub(float dd, float p, int lim, int k0, int k1) {
+  const float r = __builtin_amdgcn_rcpf(dd);
+  float lo = (p - (float)lim + 0.5f) * r, hi = (p + 0.5f) * r;
+  if (dd < 0.0f) {
+    const float t = lo;
+    lo = hi;
+    hi = t;
+  }
+  lo = fminf(fmaxf(lo - 1e-3f, -1.0e6f), 1.0e6f);
+  hi = fminf(fmaxf(hi + 1e-3f, -1.0e6f), 1.0e6f);
+  const int kl = max(k0, (int)ceilf(lo)), kh = min(k1, (int)floorf(hi));
+  return max(0, kh - kl + 1);
+}
+
 template <int RG, int FB, int NS, bool ROWB, bool RM>
 __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __restrict__ proj,
                                                              const float* __restrict__ full, int V, int W, int H,
                                                              int aw, float bl, float fuse, int z0, int z1,
-                                                             float* __restrict__ out, int y0, long PP) {
+                                                             float* __restrict__ out, int y0, long PP, int inb) {
   __shared__ RiShared S;
   __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1396,15 +1417,33 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
   int best = nd;  // smallest candidate index found stable (nd: none yet)
   int nxt = 0;    // next candidate to hand to a slot
   int k[NS], j[NS], st[NS];
+  int left[NS];     // upper bound on the in-image views the slot has still to visit
   unsigned jo[NS];  // j * P4: byte offset of view j
   float d[NS], bd[NS];
+  // inb: the walk's bounds count only views whose reprojection is inside the
+  // image (an outside one never votes): a candidate with a + (in-image views)
+  // < 0 is given up without a gather, and a slot stops once its stability is
+  // decided either way.  The camera grid is aw x (V / aw) (inb = 0 otherwise).
+  const int cr = z0 + RG * fg.g + wave;
+  const int crx = cr % aw, cry = cr / aw, ah = V / aw;
+  auto bound = [&](float dv, float bdv) {
+    return inb ? in_span_ub(dv, xf, W, -crx, aw - 1 - crx) * in_span_ub(bdv, yf, H, -cry, ah - 1 - cry) : V;
+  };
   auto take = [&](int s) {  // hand candidate nxt to slot s (k = nd: idle)
-    k[s] = nxt < best ? nxt : nd;
-    if (k[s] < nd) {
-      nxt++;
-      d[s] = S.sv[k[s]][lane];
-      st[s] = S.a[k[s]][lane];
-      bd[s] = bl * d[s];
+    k[s] = nd;
+    while (nxt < best && nxt < nd) {
+      const int c = nxt++;
+      const float dv = S.sv[c][lane];
+      const int a = S.a[c][lane];
+      const float bdv = bl * dv;
+      const int nb = bound(dv, bdv);
+      if (a + nb < 0) continue;  // unstable whatever the gathers say
+      k[s] = c;
+      d[s] = dv;
+      st[s] = a;
+      bd[s] = bdv;
+      left[s] = nb;
+      break;
     }
     j[s] = 0;
     jo[s] = 0;
@@ -1450,6 +1489,7 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
       for (int u = 0; u < FB; u++) {
         const float ad = fabsf(dc[s][u] - d[s]);
         st[s] += in[s][u] ? (ad < fuse ? 1 : 0) - (ad > fuse ? 1 : 0) : 0;
+        left[s] -= in[s][u] ? 1 : 0;
       }
       j[s] += FB;
       jo[s] += FB * P4;
@@ -1457,13 +1497,16 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
 #pragma unroll
     for (int s = 0; s < NS; s++) {
       if (k[s] >= best) continue;
-      // each remaining view adds at most +1: a candidate is given up once
-      // stab >= 0 is out of reach (stab counts exactly: this only skips work)
+      // each remaining in-image view adds +1 at most and -1 at least: the
+      // candidate is decided once stab >= 0 is out of reach or assured (stab
+      // counts exactly: this only skips work).  left never undercounts: it
+      // started at an upper bound and drops by the in-image views visited.
+      const int rem = min(V - j[s], left[s]);
       const bool fin = j[s] >= V;
-      if (fin && st[s] >= 0) {
+      if ((fin || st[s] - rem >= 0) && st[s] >= 0) {
         best = k[s];  // stable; every slot above it is dropped by the loop test
         k[s] = nd;
-      } else if (fin || st[s] + (V - j[s]) < 0) {
+      } else if (fin || st[s] + rem < 0) {
         take(s);
       }
     }
@@ -1755,16 +1798,19 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
 #define MVS_RIQ(FBV, NSV)                                                                                         \
   if (aw % FBV == 0 && rmo)                                                                                       \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true, true>), glr, dim3(64 * RG), 0, s, proj, full, V, W, \
-                       H, aw, bl, fuse, z0, z1, out, ya, PP);                                                             \
+                       H, aw, bl, fuse, z0, z1, out, ya, PP, inb);                                                        \
   else if (aw % FBV == 0)                                                                                         \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, true, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, \
-                       H, aw, bl, fuse, z0, z1, out, ya, PP);                                                             \
+                       H, aw, bl, fuse, z0, z1, out, ya, PP, inb);                                                        \
   else if (rmo)                                                                                                   \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false, true>), glr, dim3(64 * RG), 0, s, proj, full, V,   \
-                       W, H, aw, bl, fuse, z0, z1, out, ya, PP);                                                          \
+                       W, H, aw, bl, fuse, z0, z1, out, ya, PP, inb);                                                     \
   else                                                                                                            \
     hipLaunchKernelGGL((k_remove_incons_q<RG, FBV, NSV, false, false>), gl, dim3(64 * RG), 0, s, proj, full, V,   \
-                       W, H, aw, bl, fuse, z0, z1, out, ya, PP);
+                       W, H, aw, bl, fuse, z0, z1, out, ya, PP, inb);
+        // MVS_FILTER_BOUND=0 (read per call): the walk's bounds over every view (A/B)
+        const char* fbd = getenv("MVS_FILTER_BOUND");
+        const int inb = (V % aw == 0 && !(fbd && atoi(fbd) == 0)) ? 1 : 0;
         const bool rmo = !(getenv("MVS_FILTER_ORDER") && std::string(getenv("MVS_FILTER_ORDER")) == "ref");
         const dim3 glr(((W + 63) / 64) * ((z1 - z0 + RG - 1) / RG), NR);
         const char* ns = getenv("MVS_FILTER_NS");  // candidate slots per lane (1 | 2)

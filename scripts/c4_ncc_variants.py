@@ -34,10 +34,16 @@ def main():
         "v2": {z: [z - aw, z + aw]},
         "d1": {z: [z + aw + 1]},
         "knn5": {z: params.nearest_neighbours(aw, ah, 5)[z]},
+        "corner0": {0: params.nearest_neighbours(aw, ah, 5)[0]},  # a neighbour two rows away
+        "top1": {1: params.nearest_neighbours(aw, ah, 5)[1]},
+        "edge8": {8: params.nearest_neighbours(aw, ah, 5)[8]},
     }
+    if os.environ.get("CASES"):
+        cases = {k: v for k, v in cases.items() if k in os.environ["CASES"].split(",")}
     variants = [(0, 0), (8, 4), (8, 2), (4, 4), (4, 2), (4, 1)]
     res = {}
     for name, nb in cases.items():
+        z = next(iter(nb))  # the case's reference view
         lists = [nb.get(v, []) for v in range(V)]
         vs, sn = params.flatten_subsets(lists)
         cam = CameraArray(aw, 1.0, levels, vs, sn)

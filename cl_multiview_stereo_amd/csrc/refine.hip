@@ -879,46 +879,6 @@ __global__ __launch_bounds__(256) void k_proj_inv(const float* __restrict__ full
   }
   proj[PO * r + p] = md;  // PO: proj's view stride (W H, or a band's rows x W)
 }
-// The same chain for NC pixels per thread (rows y0 .. y0 + NC - 1 of one
-// column), the NC chains interleaved view by view: per view the NC gathers are
-// issued together, so a wave keeps NC independent loads in flight where
-// k_proj_inv keeps one (k_proj_inv is bound by the chain's gather latency,
-// not by the TA or L2: ~0.9 us per gather at full occupancy).
-template <int NC>
-__global__ __launch_bounds__(256) void k_proj_inv_mc(const float* __restrict__ full, int V, int W, int H, int aw,
-                                                     float bl, int z0, float* __restrict__ proj, long PO, int ya,
-                                                     int yb) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y0 = ya + blockIdx.y * NC, r = z0 + blockIdx.z;
-  if (x >= W) return;
-  const long P = (long)W * H;
-  const int crx = r % aw, cry = r / aw;
-  const float xf = (float)x;
-  float md[NC];
-#pragma unroll
-  for (int c = 0; c < NC; c++) md[c] = y0 + c < yb ? full[P * r + (long)(y0 + c) * W + x] : 0.0f;
-  for (int i = 0; i < V; i++) {
-    if (i == r) continue;
-    const float fdx = (float)(crx - i % aw), fdy = (float)(cry - i / aw);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(full + P * i), 0, 0x7fffffff, 0x00020000);
-    bool in[NC];
-    float cd[NC];
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-      const int xp = (int)(xf - round_ha(md[c] * fdx));
-      const int yp = (int)((float)(y0 + c) - round_ha((bl * md[c]) * fdy));
-      in[c] = (unsigned)xp < (unsigned)W && (unsigned)yp < (unsigned)H;
-      const int off = in[c] ? (int)((unsigned)yp * (unsigned)W + (unsigned)xp) * 4 : 0x7fffffff;
-      cd[c] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-    }
-#pragma unroll
-    for (int c = 0; c < NC; c++)
-      if (in[c] && md[c] < cd[c]) md[c] = cd[c];
-  }
-#pragma unroll
-  for (int c = 0; c < NC; c++)
-    if (y0 + c < yb) proj[PO * r + (long)(y0 + c) * W + x] = md[c];
-}
-
 __global__ void k_remove_incons(const float* __restrict__ proj, const float* __restrict__ full, int V, int W, int H,
                                 int aw, float bl, float fuse, int z0, float* __restrict__ out, int y0, long PP) {
   int x = blockIdx.x * blockDim.x + threadIdx.x, y = y0 + blockIdx.y, r = z0 + blockIdx.z;
@@ -1139,150 +1099,7 @@ __global__ __launch_bounds__(256) void k_remove_incons_px(const float* __restric
   }
 }
 
-// The same answer with the per-pixel preparation shared through LDS.  The
-// walk over candidates is a chain of dependent gather round trips, so the
-// kernel is latency-bound: k_remove_incons_px keeps 96 candidate registers
-// per thread (144 VGPRs, 3 waves per SIMD) and walks a shard's references one
-// after another.  Here a workgroup is 64 pixels of a row x RG references: the
-// reference-independent part -- the V proj values, their descending sort and
-// each candidate's first stability term -- is computed once into LDS by the
-// RG waves together, then wave w walks the candidates of reference
-// z0 + RG * blockIdx.z + w from LDS with a handful of registers.
-constexpr int RI_MAXV = 32;
-template <int RG, int FB, int CP>
-__global__ __launch_bounds__(64 * RG) void k_remove_incons_lds(const float* __restrict__ proj,
-                                                               const float* __restrict__ full, int V, int W, int H,
-                                                               int aw, float bl, float fuse, int z0, int z1,
-                                                               float* __restrict__ out, int y0, long PP) {
-  __shared__ float s_pv[RI_MAXV][64];  // proj values at the pixel, per view
-  __shared__ float s_sv[RI_MAXV][64];  // candidates sorted descending (-inf: none)
-  __shared__ float s_a[RI_MAXV][64];   // first stability term of each sorted candidate
-  __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int x = blockIdx.x * 64 + lane, y = y0 + blockIdx.y;
-  const bool xin = x < W;
-  const long P = (long)W * H, p = (long)y * W + (xin ? x : 0);
-  for (int j = wave; j < RI_MAXV; j += RG) s_pv[j][lane] = (xin && j < V) ? proj[PP * j + p] : 0.0f;
-  {
-    const int r = z0 + RG * blockIdx.z + wave;
-    if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the walk evaluates them
-      s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float sv[RI_MAXV];
-#pragma unroll
-    for (int j = 0; j < RI_MAXV; j++) {
-      const float v = s_pv[j][lane];
-      sv[j] = v != 0 ? v : -INFINITY;  // non-candidates sort last
-    }
-    sort_desc<RI_MAXV>(sv);
-#pragma unroll
-    for (int j = 0; j < RI_MAXV; j++) s_sv[j][lane] = sv[j];
-  }
-  __syncthreads();
-  for (int k = wave; k < RI_MAXV; k += RG) {
-    const float d = s_sv[k][lane];
-    float a = 0.0f;
-    for (int j = 0; j < V; j++) {
-      const float pj = s_pv[j][lane];
-      if (pj != 0) {
-        const float diff = pj - d;
-        if (fabsf(diff) > fuse) a = a - 1.0f;
-        if (fabsf(diff) <= fuse) a = a + 1.0f;
-      }
-    }
-    s_a[k][lane] = a;
-  }
-  __syncthreads();
-  const int r = z0 + RG * blockIdx.z + wave;
-  if (r >= z1 || !xin) return;  // after the last barrier
-  const float xf = (float)x, yf = (float)y;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)full, 0, 0x7fffffff, 0x00020000);
-  // the next distinct candidate (views holding the same d: one evaluation)
-  int k = 0;
-  float prev = __int_as_float(0x7fc00000);
-  auto next = [&](float& d, float& a) -> bool {
-    while (k < V) {
-      d = s_sv[k][lane];
-      a = s_a[k][lane];
-      k++;
-      if (d == -INFINITY) {  // no candidates left
-        k = V;
-        return false;
-      }
-      const bool dup = d == prev;
-      prev = d;
-      if (!dup) return true;
-    }
-    return false;
-  };
-  // CP candidates are evaluated together (their gathers in flight at once):
-  // the later ones only matter when the earlier are unstable, which is the
-  // common case; the answer is still the first stable one in order
-  float dest = 0.0f;
-  while (true) {
-    float d[CP], st[CP], bd[CP];
-    bool has[CP];
-#pragma unroll
-    for (int c = 0; c < CP; c++) {
-      has[c] = next(d[c], st[c]);
-      bd[c] = bl * d[c];
-    }
-    if (!has[0]) break;
-    for (int j0 = 0; j0 < V; j0 += FB) {
-      // each remaining view adds at most +1: a candidate stops once stab >= 0
-      // is out of reach (stab counts exactly, so this only skips work)
-      bool live[CP], any = false;
-#pragma unroll
-      for (int c = 0; c < CP; c++) {
-        live[c] = has[c] && st[c] + (float)(V - j0) >= 0.0f;
-        any = any || live[c];
-      }
-      if (!any) break;
-      float dc[CP][FB];
-      bool in[CP][FB];
-#pragma unroll
-      for (int u = 0; u < FB; u++) {
-        const int j = j0 + u;
-        const float2 o = s_off[wave][j < V ? j : 0];  // wave-uniform: an LDS broadcast
-#pragma unroll
-        for (int c = 0; c < CP; c++) {
-          const int xx = (int)(xf - roundf(d[c] * o.x));
-          const int yy = (int)(yf - roundf(bd[c] * o.y));
-          in[c][u] = live[c] && j < V && (unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H;
-          // 32-bit byte offsets (the stack is < 2 GB: the launcher checks): the view
-          // base is scalar, the in-view offset one integer multiply-add.  Every
-          // lane issues its load -- a skipped tap gets an offset past the buffer
-          // and reads 0 -- so no branch splits the block's gathers and they all
-          // stay in flight together (a branch made the compiler wait on each)
-          const int off = in[c][u] ? (yy * W + xx) * 4 : 0x7fffffff;
-          dc[c][u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, (int)(P * j * 4), 0));
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < CP; c++)
-#pragma unroll
-        for (int u = 0; u < FB; u++) {
-          if (in[c][u]) {
-            const float diff = dc[c][u] - d[c];
-            if (fabsf(diff) > fuse) st[c] = st[c] - 1.0f;
-            if (fabsf(diff) < fuse) st[c] = st[c] + 1.0f;
-          }
-        }
-    }
-    bool done = false;
-#pragma unroll
-    for (int c = 0; c < CP; c++)
-      if (!done && has[c] && st[c] >= 0) {
-        dest = d[c];
-        done = true;
-      }
-    if (done || !has[CP - 1]) break;
-  }
-  out[P * r + p] = dest;
-}
-
+constexpr int RI_MAXV = 32;  // views of the per-lane queue walk
 
 // The same answer with one work queue per lane.  k_remove_incons_lds walks
 // candidates in lock-step: a wave runs every candidate until the LAST of its
@@ -1514,147 +1331,6 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
   out[P * r + p] = best < nd ? S.sv[best][lane] : 0.0f;
 }
 
-// The same answer with the wave's work balanced over its lanes.  In
-// k_remove_incons_q a lane walks its own pixel's candidates, so a wave runs
-// as long as its slowest pixel (measured at C4: ~42 gather passes per wave
-// where a lane needs ~19 on average; the kernel is VALU-issue bound at
-// 0.8, most of it idle lanes' slots).  Here the wave's work items are the
-// (pixel, candidate) pairs of its 64 pixels, handed out in candidate-major
-// order -- every pixel's candidate 0, then every pixel's candidate 1, ... --
-// to whichever lanes are idle (ballot + mbcnt ranks, an LDS slot table).  A
-// lane walks its item's views in blocks of FB; a stable item lowers its
-// pixel's best index (LDS atomic min), and items above a pixel's best are
-// never handed out (or are dropped).  Each pixel's answer is its smallest
-// stable candidate index -- the first stable candidate in descending order,
-// as in k_remove_incons_q -- since every candidate below it was handed out
-// and proven unstable.  Measured at C4: 21.1 ms against k_remove_incons_q's
-// 18.1 (all 32 references with k_proj_inv): the hand-out rounds cost VALU/LDS
-// round trips, and lanes working other pixels' items spread a gather
-// instruction over more cache lines (the TA was already 75 % busy).  Kept as
-// an A/B option (MVS_FILTER_KERNEL=b).
-template <int RG, int FB, bool ROWB>
-__global__ __launch_bounds__(64 * RG) void k_remove_incons_b(const float* __restrict__ proj,
-                                                             const float* __restrict__ full, int V, int W, int H,
-                                                             int aw, float bl, float fuse, int z0, int z1,
-                                                             float* __restrict__ out, int y0, long PP) {
-  __shared__ RiShared S;
-  __shared__ float2 s_off[RG][RI_MAXV];  // per wave: view j's camera offset from the reference (dx, dy)
-  __shared__ int s_best[RG][64];         // per wave: smallest candidate index found stable, per pixel
-  __shared__ int s_slot[RG][64];         // per wave: hand-out table
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int x0 = blockIdx.x * 64, y = y0 + blockIdx.y;
-  const bool xin = x0 + lane < W;
-  const long P = (long)W * H, prow = (long)y * W;
-  {
-    const int r = z0 + RG * blockIdx.z + wave;
-    if (lane < RI_MAXV)  // (float)(cx - crx), (float)(cy - cry) as the reference evaluates them
-      s_off[wave][lane] = make_float2((float)(lane % aw - r % aw), (float)(lane / aw - r / aw));
-  }
-  if (wave == 0) ri_prep(S, proj, PP, prow + (xin ? x0 + lane : 0), xin, V, fuse, lane);
-  __syncthreads();
-  const int r = z0 + RG * blockIdx.z + wave;
-  if (r >= z1) return;  // whole wave, after the only barrier
-  auto wsync = [] {     // this wave's LDS writes visible to its other lanes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  int* best = s_best[wave];
-  const int ndl = S.nd[lane];  // lane as pixel: its distinct candidates
-  best[lane] = ndl;            // none stable yet
-  wsync();
-  const float yf = (float)y;
-  const unsigned P4 = (unsigned)(P * 4);  // the launcher checks V * P * 4 < 2^31
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)full, 0, 0x7fffffff, 0x00020000);
-  // this lane's item: pixel ip, candidate ik, next view j (byte offset jo)
-  bool busy = false;
-  int ip = 0, ik = 0, j = 0, st = 0;
-  unsigned jo = 0;
-  float d = 0.0f, bd = 0.0f, xf = 0.0f;
-  int ck = 0;                // hand-out round: candidate index (wave-uniform)
-  unsigned long long taken = 0;  // pixels of round ck handed out (wave-uniform)
-  while (true) {
-    unsigned long long need = __builtin_amdgcn_ballot_w64(!busy);
-    while (need != 0 && ck < RI_MAXV) {
-      const int bl_ = __hip_atomic_load(&best[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      const unsigned long long avail = __builtin_amdgcn_ballot_w64(ndl > ck && bl_ > ck) & ~taken;
-      if (avail == 0) {
-        ck++;
-        taken = 0;
-        continue;
-      }
-      const int ra = __builtin_amdgcn_mbcnt_hi((unsigned)(avail >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)avail, 0));
-      const int rn = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0));
-      const int na = __builtin_popcountll(avail), nn = __builtin_popcountll(need);
-      if ((avail >> lane) & 1ull) s_slot[wave][ra] = lane;
-      wsync();
-      if (!busy && rn < na) {
-        ip = s_slot[wave][rn];
-        ik = ck;
-        busy = true;
-        d = S.sv[ck][ip];
-        st = S.a[ck][ip];
-        bd = bl * d;
-        xf = (float)(x0 + ip);
-        j = 0;
-        jo = 0;
-      }
-      taken |= __builtin_amdgcn_ballot_w64(((avail >> lane) & 1ull) && ra < nn);
-      need = __builtin_amdgcn_ballot_w64(!busy);
-      wsync();  // the slot table is rewritten by the next round
-    }
-    if (__builtin_amdgcn_ballot_w64(busy) == 0) break;  // nothing in flight, nothing left
-    if (busy) {
-      float dc[FB];
-      bool in[FB];
-      if (ROWB) {
-        const float2 o = s_off[wave][j];
-        const int yy = (int)(yf - round_ha(bd * o.y));
-        const bool yok = (unsigned)yy < (unsigned)H;
-        const unsigned ro = jo + __umul24((unsigned)yy, (unsigned)W) * 4u;
-#pragma unroll
-        for (int u = 0; u < FB; u++) {
-          const int xx = (int)(xf - round_ha(d * (o.x + (float)u)));
-          in[u] = yok && j + u < V && (unsigned)xx < (unsigned)W;
-          const int off = in[u] ? (int)(ro + (unsigned)u * P4 + (unsigned)xx * 4u) : 0x7fffffff;
-          dc[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < FB; u++) {
-          const float2 o = s_off[wave][min(j + u, V - 1)];
-          const int xx = (int)(xf - round_ha(d * o.x));
-          const int yy = (int)(yf - round_ha(bd * o.y));
-          in[u] = j + u < V && (unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H;
-          const int off =
-              in[u] ? (int)(jo + (unsigned)u * P4 + (__umul24((unsigned)yy, (unsigned)W) + (unsigned)xx) * 4u) : 0x7fffffff;
-          dc[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < FB; u++) {
-        const float ad = fabsf(dc[u] - d);
-        st += in[u] ? (ad < fuse ? 1 : 0) - (ad > fuse ? 1 : 0) : 0;
-      }
-      j += FB;
-      jo += FB * P4;
-      const bool fin = j >= V;
-      if (fin && st >= 0) {
-        __hip_atomic_fetch_min(&best[ip], ik, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        busy = false;
-      } else if (fin || st + (V - j) < 0 ||
-                 __hip_atomic_load(&best[ip], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) < ik) {
-        busy = false;  // unstable, or a smaller candidate of the pixel is stable
-      }
-    }
-    wsync();
-  }
-  if (xin) {
-    const int b = best[lane];
-    out[P * r + prow + x0 + lane] = b < ndl ? S.sv[b][lane] : 0.0f;
-  }
-}
-
 }  // namespace
 
 int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
@@ -1710,21 +1386,8 @@ int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const 
   // band: proj holds rows [ya, yb) only, [V][yb - ya][W] (as launch_remove_incons)
   const long PO = band ? (long)NR * W : (long)W * H;
   if (band) proj -= (long)ya * W;
-  // MVS_PROJ_NC (read per call): pixels (rows) per thread, 1 = k_proj_inv
-  const char* nce = getenv("MVS_PROJ_NC");
-  const int nc = nce ? atoi(nce) : 1;
-  if (nc == 2)
-    hipLaunchKernelGGL(k_proj_inv_mc<2>, dim3((W + 255) / 256, (NR + 1) / 2, z1 - z0), dim3(256), 0, s, full, V, W, H,
-                       aw, bl, z0, proj, PO, ya, yb);
-  else if (nc == 4)
-    hipLaunchKernelGGL(k_proj_inv_mc<4>, dim3((W + 255) / 256, (NR + 3) / 4, z1 - z0), dim3(256), 0, s, full, V, W, H,
-                       aw, bl, z0, proj, PO, ya, yb);
-  else if (nc == 8)
-    hipLaunchKernelGGL(k_proj_inv_mc<8>, dim3((W + 255) / 256, (NR + 7) / 8, z1 - z0), dim3(256), 0, s, full, V, W, H,
-                       aw, bl, z0, proj, PO, ya, yb);
-  else
-    hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, NR, z1 - z0), dim3(256), 0, s, full, V, W, H, aw, bl, z0,
-                       proj, PO, ya);
+  hipLaunchKernelGGL(k_proj_inv, dim3((W + 255) / 256, NR, z1 - z0), dim3(256), 0, s, full, V, W, H, aw, bl, z0, proj,
+                     PO, ya);
   MVS_LAUNCH_CHECK("k_proj_inv");
   return 0;
 }
@@ -1751,48 +1414,16 @@ int launch_remove_incons(hipStream_t s, int V, int W, int H, int aw, float bl, f
                          out, ya, PP);
     else if (V <= 32 && (long)V * W * H * 4 < (1L << 31) &&
              !(getenv("MVS_FILTER_KERNEL") && std::string(getenv("MVS_FILTER_KERNEL")) == "px")) {
-      // 32-bit gather offsets.  Default: one work queue per lane
-      // (k_remove_incons_q, MVS_FILTER_NS candidates at once);
-      // MVS_FILTER_KERNEL=b: the wave's (pixel, candidate) items balanced over
-      // its lanes, =lds: the lock-step walk (MVS_FILTER_CP candidates
-      // together), =px: the per-pixel form below.  MVS_FILTER_FB (read per
-      // call): views per gather block.  Measured at C4, all 32 references
-      // with k_proj_inv (scripts/bench_filter.py): q 18.1 ms (NS 2, FB 2),
-      // b 21.1 ms (FB 2), lds 27.9 ms.
+      // 32-bit gather offsets: one work queue per lane (k_remove_incons_q,
+      // MVS_FILTER_NS candidates at once, MVS_FILTER_FB views per gather block,
+      // both read per call); MVS_FILTER_KERNEL=px: the per-pixel form below.
+      // Measured at C4, all 32 references with k_proj_inv
+      // (scripts/bench_filter.py): q 18.1 ms (NS 2, FB 2); the lane-balanced
+      // hand-out of (pixel, candidate) items 21.1 ms and the lock-step walk
+      // 27.9 ms (both removed in round 3).
       constexpr int RG = 4;
       const dim3 gl((W + 63) / 64, NR, (z1 - z0 + RG - 1) / RG);
-      const char* fk = getenv("MVS_FILTER_KERNEL");
-      if (fk && std::string(fk) == "lds") {
-        const char* cp = getenv("MVS_FILTER_CP");
-        const int ncp = cp ? atoi(cp) : 2;
-        if (ncp == 1)
-          hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 1>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
-                             fuse, z0, z1, out, ya, PP);
-        else if (ncp == 3)
-          hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 3>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
-                             fuse, z0, z1, out, ya, PP);
-        else
-          hipLaunchKernelGGL((k_remove_incons_lds<RG, 4, 2>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,
-                             fuse, z0, z1, out, ya, PP);
-      } else if (fk && std::string(fk) == "b") {
-        const char* fb = getenv("MVS_FILTER_FB");
-        const int nfb = fb ? atoi(fb) : 4;
-#define MVS_RIB(FBV)                                                                                              \
-  if (aw % FBV == 0)                                                                                              \
-    hipLaunchKernelGGL((k_remove_incons_b<RG, FBV, true>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl,  \
-                       fuse, z0, z1, out, ya, PP);                                                                        \
-  else                                                                                                            \
-    hipLaunchKernelGGL((k_remove_incons_b<RG, FBV, false>), gl, dim3(64 * RG), 0, s, proj, full, V, W, H, aw, bl, \
-                       fuse, z0, z1, out, ya, PP);
-        if (nfb == 2) {
-          MVS_RIB(2)
-        } else if (nfb == 8) {
-          MVS_RIB(8)
-        } else {
-          MVS_RIB(4)
-        }
-#undef MVS_RIB
-      } else {
+      {
         const char* fb = getenv("MVS_FILTER_FB");
         const int nfb = fb ? atoi(fb) : 2;
 #define MVS_RIQ(FBV, NSV)                                                                                         \

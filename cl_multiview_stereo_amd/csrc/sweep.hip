@@ -11,7 +11,7 @@
 //                    level pair a lane forms its column's absolute differences
 //                    and the 25-tap sums run in the reference's order as
 //                    v_pk_add_f32 over the two levels, the window columns
-//                    passed lane to lane by DPP wave_shr (SYS, the default)
+//                    passed lane to lane by DPP wave_shr (systolic)
 //                    or through an LDS plane (the first, two-phase form).
 //  k_sweep_pixel_sad the first per-pixel form (every (d, neighbour) region
 //                    gathered from global memory): kept for level sets with
@@ -250,7 +250,6 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
 // level order; the 4 waves' (cost, level) winners are merged
 // lexicographically at the end.
 constexpr int SB_TW = 60;   // output columns per tile
-constexpr int SB_ADW = 68;  // AD plane pitch (float2): lanes 60..63 read up to column 67
 constexpr int SB_NBLK = 2;  // 64-column blocks per band row (band columns <= 128)
 constexpr float SB_INIT = 1000000.0f;
 // row-table entry of a row outside the image: a valid entry (yp-by0)*bw - bx0
@@ -296,31 +295,30 @@ __device__ __forceinline__ float shr1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 
-// MODE 0: register-staged band prefetch (default); 1: load + store the band at
-// the start of its own step (no overlap; A/B reference).
-// SYS: phase B as a systolic chain across lanes instead of through LDS.  An
-// output's 25-tap chain takes its 5 window columns in order (x offset outer),
+// The 25-tap sums run as a systolic chain across lanes (round 2's two-phase
+// form staged the AD plane in LDS per wave and re-read it per tap: 3.35 ms
+// per C2 view against 2.42; it was removed in round 3 with the other A/B
+// variants).  An output's 25-tap chain takes its 5 window columns in order (x offset outer),
 // and window column i of output x is region column x-2+i = lane (x-x0)+i.  So
 // every lane runs the 5-row inner chains of its OWN column's taps (kept in
 // registers) on the partial sums it receives from the lane to its left
 // (DPP wave_shr:1, folded into the first add of each column): after the 5th
 // column, lane l holds the output of image column x0 + l - 4.  The AD plane,
 // its LDS writes/reads and the wave barriers of the two-phase form disappear.
-// AFF (SYS only): every level's row shift is integral, so region row r of
+// AFF: every level's row shift is integral, so region row r of
 // level j reads band row r + (y0 - 2 - fdy_j - by0) exactly and is valid on
 // one interval of r: the rows are addressed by immediate offsets r * BWT from
 // one per-level lane address, and validity is a scalar interval test -- no
 // row table reads, no per-row address arithmetic or compares.  BWT = the band
 // pitch (a.bw) as a compile-time constant (0: runtime, the table path).
-template <int TH, int PPW, int MODE, bool SYS = false, bool AFF = false, int BWT = 0>
+template <int TH, int PPW, bool AFF = false, int BWT = 0>
 __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab, const float* __restrict__ levels,
                                                   const SadRec* __restrict__ plan, SadArgs a,
                                                   float* __restrict__ disp) {
   constexpr int RR = TH + 4, DC = 8 * PPW;
   extern __shared__ __align__(16) uint8_t smem[];
-  float4* band = (float4*)smem;                                 // [2][brows][bw]
-  float2* adb = (float2*)(band + 2 * a.brows * a.bw);           // [4 waves][RR][SB_ADW] (two-phase form only)
-  int* rtab = SYS ? (int*)adb : (int*)(adb + 4 * RR * SB_ADW);  // [2][DC][RR]
+  float4* band = (float4*)smem;                // [2][brows][bw]
+  int* rtab = (int*)(band + 2 * a.brows * a.bw);  // [2][DC][RR] (the row-table form)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware tile map (as k_ncc_volume): each XCD a contiguous strip of tiles
   const int bid = blockIdx.x, grp = bid & 7;
@@ -344,7 +342,6 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
       rb[r] = c.z;
     }
   }
-  float2* myad = adb + wave * RR * SB_ADW;
   const int T = a.nch * a.nn;
 
   SadBand pg{0, 0, 0, 0};
@@ -400,14 +397,9 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
   }
   __syncthreads();
   for (int t = 0; t < T; t++) {
-    if (MODE == 1 && t > 0) {
-      stage(t, t & 1);
-      commit(t, t & 1);
-      __syncthreads();
-    }
     // step t+1's band lands in the other buffer (last read in step t-1, before
     // the previous barrier) while this step computes
-    if (MODE == 0 && t + 1 < T) stage(t + 1, (t + 1) & 1);
+    if (t + 1 < T) stage(t + 1, (t + 1) & 1);
     const int c = t / a.nn, n = t - c * a.nn;
     if (n == 0) {
 #pragma unroll
@@ -456,65 +448,32 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
         float d1 = fabsf(rL[r] - n1.x) + fabsf(ra[r] - n1.y);
         d1 = d1 + fabsf(rb[r] - n1.z);
         ad[r] = f32x2{v0 ? d0 : 30.0f, v1 ? d1 : 30.0f};
-        if (!SYS) myad[r * SB_ADW + lane] = make_float2(ad[r].x, ad[r].y);
       }
       }
-      if (SYS) {
-        // B'. systolic: column 0 starts the chains (first tap: ((0+30)-30)+a = a
-        // exactly), columns 1..4 continue the left neighbour's partials
-        f32x2 p[TH];
-#pragma unroll
-        for (int o = 0; o < TH; o++) {
-          p[o] = ad[o];
-#pragma unroll
-          for (int jj = 1; jj < 5; jj++) p[o] = ((p[o] + k30) - k30) + ad[o + jj];
-        }
-#pragma unroll
-        for (int i = 1; i < 5; i++)
-#pragma unroll
-          for (int o = 0; o < TH; o++) {
-            f32x2 v = f32x2{shr1(p[o].x) + 30.0f, shr1(p[o].y) + 30.0f};
-            v = (v - k30) + ad[o];
-#pragma unroll
-            for (int jj = 1; jj < 5; jj++) v = ((v + k30) - k30) + ad[o + jj];
-            p[o] = v;
-          }
-#pragma unroll
-        for (int o = 0; o < TH; o++) {
-          mn[q][o].x = fminf(mn[q][o].x, p[o].x);
-          mn[q][o].y = fminf(mn[q][o].y, p[o].y);
-        }
-        continue;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // B. 25-tap sums: x offset outer, y offset inner (clcode.cl:1017-1047
-      // order per output); the TH outputs' chains interleave
-      f32x2 acc[TH];
-#pragma unroll
-      for (int o = 0; o < TH; o++) acc[o] = f32x2{0.0f, 0.0f};
-#pragma unroll
-      for (int i = 0; i < 5; i++) {
-        f32x2 col[RR];
-#pragma unroll
-        for (int r = 0; r < RR; r++) {
-          const float2 v = myad[r * SB_ADW + lane + i];
-          col[r] = f32x2{v.x, v.y};
-        }
-#pragma unroll
-        for (int jj = 0; jj < 5; jj++)
-#pragma unroll
-          for (int o = 0; o < TH; o++) acc[o] = ((acc[o] + k30) - k30) + col[o + jj];
-      }
+      // B'. systolic: column 0 starts the chains (first tap: ((0+30)-30)+a = a
+      // exactly), columns 1..4 continue the left neighbour's partials
+      f32x2 p[TH];
 #pragma unroll
       for (int o = 0; o < TH; o++) {
-        mn[q][o].x = fminf(mn[q][o].x, acc[o].x);
-        mn[q][o].y = fminf(mn[q][o].y, acc[o].y);
+        p[o] = ad[o];
+#pragma unroll
+        for (int jj = 1; jj < 5; jj++) p[o] = ((p[o] + k30) - k30) + ad[o + jj];
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int i = 1; i < 5; i++)
+#pragma unroll
+        for (int o = 0; o < TH; o++) {
+          f32x2 v = f32x2{shr1(p[o].x) + 30.0f, shr1(p[o].y) + 30.0f};
+          v = (v - k30) + ad[o];
+#pragma unroll
+          for (int jj = 1; jj < 5; jj++) v = ((v + k30) - k30) + ad[o + jj];
+          p[o] = v;
+        }
+#pragma unroll
+      for (int o = 0; o < TH; o++) {
+        mn[q][o].x = fminf(mn[q][o].x, p[o].x);
+        mn[q][o].y = fminf(mn[q][o].y, p[o].y);
+      }
     }
     if (n == a.nn - 1) {  // chunk complete: first-minimum WTA in level order
 #pragma unroll
@@ -535,7 +494,7 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
     }
     // step t+1's row table (its rows were last read in step t-1); the barrier
     // (vmcnt(0) first) publishes the table and the landed band
-    if (MODE == 0 && t + 1 < T && !AFF) commit(t + 1, (t + 1) & 1);
+    if (t + 1 < T && !AFF) commit(t + 1, (t + 1) & 1);
     __syncthreads();
   }
   // merge the 4 waves' winners: lexicographic (cost, level)
@@ -549,8 +508,8 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
   __syncthreads();
   for (int k = tid; k < TH * 64; k += 256) {
     const int o = k >> 6, l = k & 63;
-    const int x = SYS ? x0 + l - 4 : x0 + l, y = y0 + o;  // SYS: lane l holds column x0 + l - 4
-    if ((SYS ? l < 4 : l >= SB_TW) || x >= W || y >= H) continue;
+    const int x = x0 + l - 4, y = y0 + o;  // lane l holds column x0 + l - 4
+    if (l < 4 || x >= W || y >= H) continue;
     float bv = mb[k];
     int bi = mi[k];
 #pragma unroll
@@ -847,10 +806,10 @@ namespace {
 // Band-staged SAD sweep: host plan + launch for one reference view.  Returns 1
 // when the level set has fractional column shifts or the bands do not fit
 // the LDS (the caller then uses k_sweep_pixel_sad).
-template <int TH, int PPW, int MODE = 0, bool SYS = false>
+template <int TH, int PPW>
 int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
                       const int* vs_host, const int* sn_host, int aw, float bl, int z, float* disp) {
-  bool aff = SYS && MODE == 0 && getenv("MVS_SAD_AFF") == nullptr;  // MVS_SAD_AFF set: the table path (A/B)
+  bool aff = getenv("MVS_SAD_AFF") == nullptr;  // MVS_SAD_AFF set: the row-table path (A/B)
   constexpr int RR = TH + 4, DC = 8 * PPW;
   const int nn = sn_host[z];
   const int nch = (D + DC - 1) / DC;
@@ -896,8 +855,7 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
   // truncated ends differ by < RR + span_y); one spare row for the float
   // rounding of fractional shifts, none when every shift is integral
   a.brows = RR + (int)std::ceil(span_y) + (aff ? 0 : 1);
-  const size_t lds = 16 * 2 * (size_t)a.brows * a.bw + (SYS ? 0 : 8 * 4 * (size_t)RR * SB_ADW) +
-                     (aff ? 0 : 4 * 2 * (size_t)DC * RR);
+  const size_t lds = 16 * 2 * (size_t)a.brows * a.bw + (aff ? 0 : 4 * 2 * (size_t)DC * RR);
   // band columns: SB_NBLK pieces of 64 at most (the systolic tile's reach)
   if (a.bw > 64 * SB_NBLK) return 1;
   if (lds > 160 * 1024 || (size_t)4 * TH * 64 * 8 > 16 * 2 * (size_t)a.brows * a.bw) return 1;
@@ -907,10 +865,8 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
   a.tiles_x = (W + SB_TW - 1) / SB_TW;
   a.ntiles = a.tiles_x * ((H + TH - 1) / TH);
   a.tiles_per_xcd = (a.ntiles + 7) / 8;
-  auto kern = k_sad_band<TH, PPW, MODE, SYS>;
-  if constexpr (SYS && MODE == 0) {
-    if (aff) kern = a.bw == 64 ? k_sad_band<TH, PPW, MODE, SYS, true, 64> : k_sad_band<TH, PPW, MODE, SYS, true, 128>;
-  }
+  auto kern = k_sad_band<TH, PPW>;
+  if (aff) kern = a.bw == 64 ? k_sad_band<TH, PPW, true, 64> : k_sad_band<TH, PPW, true, 128>;
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(sad lds)");
@@ -924,11 +880,10 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
 
 int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, const float* levels_host, int D,
                            const int* vs_host, const int* sn_host, int aw, float bl, int z0, int z1, float* disp) {
-  // MVS_SAD_KERNEL: "sys8x2", "sys8", "sys16", "band8", "band8x2", "band16",
-  // "band8s", "gather" (A/B and tests).  Without it: the systolic kernel with
-  // 16-level chunks, else with 8-level chunks (taller bands: vertical
-  // neighbours), else the gather kernel.  A band variant named explicitly never
-  // falls back (MVS_E_UNSUPPORTED), so a test of it cannot pass on another.
+  // MVS_SAD_KERNEL: "sys8x2", "sys8", "gather" (A/B and tests).  Without it:
+  // 16-level chunks, else 8-level chunks (taller bands: vertical neighbours),
+  // else the gather kernel.  A band variant named explicitly never falls back
+  // (MVS_E_UNSUPPORTED), so a test of it cannot pass on another.
   const char* kv = getenv("MVS_SAD_KERNEL");
   const std::string kind = kv ? kv : "auto";
   const bool strict = kv != nullptr && kind != "gather";
@@ -937,23 +892,12 @@ int launch_sweep_pixel_sad(mvs_ctx* ctx, int V, int W, int H, const float* lab, 
     float* out = disp + (long)(z - z0) * P;
     int rc = 1;
     if (kind == "auto") {
-      rc = launch_sad_band_t<8, 2, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
-      if (rc == 1)
-        rc = launch_sad_band_t<8, 1, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
-    } else if (kind == "band8")
-      rc = launch_sad_band_t<8, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
-    else if (kind == "band8x2")
       rc = launch_sad_band_t<8, 2>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
-    else if (kind == "band8s")
-      rc = launch_sad_band_t<8, 1, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
-    else if (kind == "band16")
-      rc = launch_sad_band_t<16, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
-    else if (kind == "sys8")
-      rc = launch_sad_band_t<8, 1, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+      if (rc == 1) rc = launch_sad_band_t<8, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+    } else if (kind == "sys8")
+      rc = launch_sad_band_t<8, 1>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
     else if (kind == "sys8x2")
-      rc = launch_sad_band_t<8, 2, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
-    else if (kind == "sys16")
-      rc = launch_sad_band_t<16, 1, 0, true>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
+      rc = launch_sad_band_t<8, 2>(ctx, V, W, H, lab, levels_host, D, vs_host, sn_host, aw, bl, z, out);
     if (rc < 0) return rc;
     if (rc == 1 && strict) {
       set_error("k_sad_band variant " + kind + " cannot stage this geometry (MVS_SAD_KERNEL set explicitly)");

@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_sad.py tests/test_gpu_ncc_c
   --timeout-method thread -p no:cacheprovider > gpurun_out/sad/tests.log 2>&1
 rc=$?; tail -5 gpurun_out/sad/tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for k in ${KINDS:-band8 band8s band8x2 band16 gather}; do
+for k in ${KINDS:-sys8x2 sys8 gather}; do
   MVS_SAD_KERNEL=$k timeout -k 10 200 python bench.py --config c2 --cost sad --steps 3 --warmup 1 --no-cpu-baseline \
     --no-sharded > gpurun_out/sad/b_$k.json 2> gpurun_out/sad/b_$k.err || exit $?
   python -c "import json;j=json.load(open('gpurun_out/sad/b_$k.json'));print('$k',j['ms_per_step'],j['value'])"

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Cross-view filter at C4 (32 views, 8x4 array, 1080p): the refined
 disparity maps of the C4 pipeline are computed once, then the filter
-(k_proj_inv + k_remove_incons_px) is timed for the whole array and for one
+(k_proj_inv + the removal kernel) is timed for the whole array and for one
 4-view shard, per variant (env knobs read per call), interleaved rounds.
 Every variant's output is compared bit-for-bit with the first one's.
 Prints one JSON dict of {variant: [min ms, median ms]}."""
@@ -20,7 +20,7 @@ from cl_multiview_stereo_amd.pipeline import Pipeline  # noqa: E402
 
 
 def main():
-    variants = sys.argv[1:] or ["MVS_FILTER_KERNEL=px", "MVS_FILTER_KERNEL=lds"]
+    variants = sys.argv[1:] or ["MVS_FILTER_KERNEL=q", "MVS_FILTER_KERNEL=px"]
     aw, ah, W, H = 8, 4, 1920, 1080
     e = Engine(0)
     st = params.Settings(spixl_size=32, array_width=aw, array_height=ah, min_disp=0, max_disp=127, inc=1, neib_hor=0,

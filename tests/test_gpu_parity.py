@@ -315,16 +315,16 @@ def test_filter_many_views(engine, aw, ah):
     assert_bits(out.cpu().numpy(), oout, "filter output")
 
 
-@pytest.mark.parametrize("kern,fb,ns", [("b", 2, 0), ("b", 4, 0), ("b", 8, 0), ("q", 2, 2), ("q", 4, 2), ("q", 2, 1),
-                                         ("q", 4, 1), ("lds", 4, 0), ("px", 4, 0), ("px", 2, 0)])
+@pytest.mark.parametrize("kern,fb,ns,bound", [("q", 2, 2, 1), ("q", 4, 2, 1), ("q", 2, 1, 1), ("q", 4, 1, 1),
+                                               ("q", 2, 2, 0), ("px", 4, 0, 1), ("px", 2, 0, 1)])
 @pytest.mark.parametrize("aw,ah", [(8, 4), (6, 5), (5, 5)])
-def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns):
+def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns, bound):
     # every removal kernel for 16 < V <= 32, forced per call (MVS_FILTER_KERNEL /
-    # _FB / _NS are read at each launch): the wave-balanced walk and the
-    # per-lane queue walk (1 or 2 candidate slots), each with row-shared
-    # (aw % FB == 0) and per-view offsets, the lock-step walk and the
-    # per-pixel form.  Near-equal candidates in long runs reach the queue
-    # kernel's full-count fallback of the first stability term.
+    # _FB / _NS / _BOUND are read at each launch): the per-lane queue walk (1
+    # or 2 candidate slots, with and without the in-image bounds), with
+    # row-shared (aw % FB == 0) and per-view offsets, and the per-pixel form.
+    # Near-equal candidates in long runs reach the queue kernel's full-count
+    # fallback of the first stability term.
     V, H, W = aw * ah, 20, 72
     rng = np.random.default_rng(aw * 100 + ah * 7 + fb)
     base = rng.integers(2, 12, size=(V, 1, 1)).astype(np.float32)
@@ -334,21 +334,21 @@ def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns):
     monkeypatch.setenv("MVS_FILTER_KERNEL", kern)
     monkeypatch.setenv("MVS_FILTER_FB", str(fb))
     monkeypatch.setenv("MVS_FILTER_NS", str(ns))
+    monkeypatch.setenv("MVS_FILTER_BOUND", str(bound))
     proj, out = engine.filter(dev(disp), aw, 1.0359, 1.0)
     oproj, oout = orc.filt(disp, aw, 1.0359, 1.0)
     assert_bits(proj.cpu().numpy(), oproj, "filter projection")
     assert_bits(out.cpu().numpy(), oout, f"filter output ({kern}, FB {fb})")
 
 
-@pytest.mark.parametrize("kern", ["q", "b", "lds", "px"])
+@pytest.mark.parametrize("kern", ["q", "px"])
 @pytest.mark.parametrize("aw,ah", [(3, 2), (4, 3), (8, 4), (9, 5), (10, 7)])
 def test_filter_row_bands(engine, monkeypatch, aw, ah, kern):
     # mvs_proj_inv_rows_d / mvs_remove_inconsistency_rows_d (the sharded
     # pipeline's banded proj all-gather): uneven row bands, every band written
     # into shared proj / out buffers, tile the full-range result for every
     # removal kernel (V = 6, 12, 32, 45, 70; the 16 < V <= 32 kernels forced
-    # per call) and every projection variant (MVS_PROJ_NC rows per thread,
-    # bands not a multiple of it)
+    # per call), the projection into the full stack and into band buffers
     V, H, W = aw * ah, 23, 70
     if kern != "q" and V != 32:
         pytest.skip("removal kernel variants apply at 16 < V <= 32")
@@ -360,17 +360,15 @@ def test_filter_row_bands(engine, monkeypatch, aw, ah, kern):
     monkeypatch.setenv("MVS_FILTER_KERNEL", kern)
     oproj, oout = orc.filt(disp, aw, 1.0359, 1.0)
     bands = [(0, 5), (5, 6), (6, 17), (17, 17), (17, 23)]
-    for nc in ("1", "2", "4", "8"):
-        monkeypatch.setenv("MVS_PROJ_NC", nc)
-        proj = torch.full((V, H, W), float("nan"), device=d.device)
+    proj = torch.full((V, H, W), float("nan"), device=d.device)
+    for ya, yb in bands:
+        engine.proj_inv(d, aw, 1.0359, 0, V, proj=proj, rows=(ya, yb))
+    assert_bits(proj.cpu().numpy(), oproj, "banded projection")
+    for z0, z1 in ((0, V // 3), (V // 3, V)):  # straight into band buffers, [V, yb - ya, W]
         for ya, yb in bands:
-            engine.proj_inv(d, aw, 1.0359, 0, V, proj=proj, rows=(ya, yb))
-        assert_bits(proj.cpu().numpy(), oproj, f"banded projection (NC {nc})")
-        for z0, z1 in ((0, V // 3), (V // 3, V)):  # straight into band buffers, [V, yb - ya, W]
-            for ya, yb in bands:
-                buf = torch.full((V, yb - ya, W), float("nan"), device=d.device)
-                engine.proj_inv(d, aw, 1.0359, z0, z1, proj=buf, rows=(ya, yb), band=True)
-                assert_bits(buf[z0:z1].cpu().numpy(), oproj[z0:z1, ya:yb], f"band-buffer projection (NC {nc})")
+            buf = torch.full((V, yb - ya, W), float("nan"), device=d.device)
+            engine.proj_inv(d, aw, 1.0359, z0, z1, proj=buf, rows=(ya, yb), band=True)
+            assert_bits(buf[z0:z1].cpu().numpy(), oproj[z0:z1, ya:yb], "band-buffer projection")
     for band in (False, True):  # proj rows within the full stack / the band alone, [V, yb - ya, W]
         out = torch.full((V, H, W), -1.0, device=d.device)
         for z0, z1 in ((0, V // 3), (V // 3, V)):

@@ -78,14 +78,9 @@ def test_sad_ties_and_no_neighbours(engine):
 # explicitly named band variant never falls back to the gather kernel
 # (MVS_E_UNSUPPORTED instead), so each case runs the kernel it names.
 _VARIANTS = {
-    "band8": (3, 3, 1, 1, 1.0359),    # vertical shifts: 22 band rows
-    "band8s": (3, 3, 1, 1, 1.0359),
-    "band8x2": (3, 1, 2, 0, 1.0),     # 16-level chunks: horizontal only
-    "band16": (3, 1, 2, 0, 1.0),      # 16-row tiles: horizontal only
+    "sys8": (3, 3, 1, 1, 1.0359),    # 8-level chunks, fractional vertical shifts (row table)
+    "sys8x2": (3, 1, 2, 0, 1.0),     # 16-level chunks (affine rows)
     "gather": (3, 3, 1, 1, 1.0359),
-    "sys8": (3, 3, 1, 1, 1.0359),     # systolic (DPP) column chain
-    "sys8x2": (3, 1, 2, 0, 1.0),
-    "sys16": (3, 1, 2, 0, 1.0),
 }
 
 
@@ -115,10 +110,10 @@ def test_sad_affine_rows(engine, monkeypatch, aw, ah, nh, nv, table):
 
 
 def test_sad_explicit_variant_does_not_fall_back(engine, monkeypatch):
-    """band8x2 cannot stage a neighbour 5 cameras away (16 levels x 5 px = 75
+    """sys8x2 cannot stage a neighbour 5 cameras away (16 levels x 5 px = 75
     columns of shift: a band wider than its 128 columns): named explicitly it
     fails loudly instead of running the gather kernel."""
-    monkeypatch.setenv("MVS_SAD_KERNEL", "band8x2")
+    monkeypatch.setenv("MVS_SAD_KERNEL", "sys8x2")
     stack, _ = synth.make_stack(140, 50, 6, 1, 0, 20, 1.0, 12)
     lab, _ = engine.cvt(torch.from_numpy(stack).cuda())
     with pytest.raises(Exception, match="cannot stage"):

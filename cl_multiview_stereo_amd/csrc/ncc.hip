@@ -458,32 +458,41 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   const long zo = (long)a.z[ref] * Pv;
   const int xc = min(x, W - 1);
   unsigned qlo[NR], qhi[NR];
-  int rsum[NR], rsq[NR];
+  int rsum[NR];
 #pragma unroll
   for (int k = 0; k < NR; k++) {
     const uint2 v = pk[zo + pair_index(min(max(y0 - R + k, 0), H - 1), xc, W)];
     qlo[k] = v.x;
     qhi[k] = v.y & HI_MASK;
     rsum[k] = dot4(qlo[k], 0x01010101u, dot4(qhi[k], 0x01010101u, 0));
-    rsq[k] = dot4(qlo[k], qlo[k], dot4(qhi[k], qhi[k], 0));
   }
   f32x2 rsn[TH / 2];  // -Sr' of output rows (2m, 2m+1)
 #pragma unroll
   for (int o = 0; o < TH; o++) {
-    int s1 = 0, s2 = 0;
+    int s1 = 0;
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-      s1 += rsum[o + k];
-      s2 += rsq[o + k];
-    }
-    const int y = y0 + o;
-    const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
-    const int var = NK * s2 - s1 * s1;
-    // fused: only wave 0 needs s_r (it publishes it in LDS), so the other
-    // waves skip the correctly rounded sqrt + divide of every row
-    if (!FUSE || wave == 0)
-      sr[o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
+    for (int k = 0; k < K; k++) s1 += rsum[o + k];
     rsn[o >> 1][o & 1] = -(float)s1;
+  }
+  // fused: only wave 0 needs s_r (it publishes it in LDS), so the other waves
+  // skip the squares and the correctly rounded sqrt + divide of every row
+  if (!FUSE || wave == 0) {
+    int rsq[NR];
+#pragma unroll
+    for (int k = 0; k < NR; k++) rsq[k] = dot4(qlo[k], qlo[k], dot4(qhi[k], qhi[k], 0));
+#pragma unroll
+    for (int o = 0; o < TH; o++) {
+      int s1 = 0, s2 = 0;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        s1 += rsum[o + k];
+        s2 += rsq[o + k];
+      }
+      const int y = y0 + o;
+      const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
+      const int var = NK * s2 - s1 * s1;
+      sr[o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
+    }
   }
   if (FUSE && wave == 0) {
 #pragma unroll

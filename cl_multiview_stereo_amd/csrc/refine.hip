@@ -1101,8 +1101,8 @@ __global__ __launch_bounds__(256) void k_remove_incons_px(const float* __restric
 
 constexpr int RI_MAXV = 32;  // views of the per-lane queue walk
 
-// The same answer with one work queue per lane.  k_remove_incons_lds walks
-// candidates in lock-step: a wave runs every candidate until the LAST of its
+// The same answer with one work queue per lane.  The round-2 lock-step form
+// (removed) walked candidates together: a wave runs every candidate until the LAST of its
 // 64 lanes has given it up, so it pays, per candidate, the longest of the 64
 // walks (measured at C4: 31.4 candidate rounds per wave against 20.5 per
 // pixel, and most of a round's gather blocks idle).  Here each lane carries

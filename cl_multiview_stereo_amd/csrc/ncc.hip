@@ -385,23 +385,23 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // -inf * 0 and of an invalid reference window); partial tiles/chunks masked
   auto store = [&](int c) {
     if (x >= W) return;
+    float srv[TH];  // FUSE: s_r of the tile's rows, read once per chunk
+    if (FUSE) {
+      const int ln = lane_now();
+#pragma unroll
+      for (int o = 0; o < TH; o += 4) {
+        const f32x4 t = *(const f32x4*)(srl + ln * TH + o);
+        srv[o] = t.x;
+        srv[o + 1] = t.y;
+        srv[o + 2] = t.z;
+        srv[o + 3] = t.w;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < DPW; j++) {
       const int dl = c * DC + wave + NW * j;
       if (dl >= a.D) break;
       if (FUSE) {
-        float srv[TH];
-        {
-          const int ln = lane_now();
-#pragma unroll
-          for (int o = 0; o < TH; o += 4) {
-            const f32x4 t = *(const f32x4*)(srl + ln * TH + o);
-            srv[o] = t.x;
-            srv[o + 1] = t.y;
-            srv[o + 2] = t.z;
-            srv[o + 3] = t.w;
-          }
-        }
 #pragma unroll
         for (int o = 0; o < TH; o += 2) {
           const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{srv[o], srv[o + 1]};

@@ -289,11 +289,6 @@ __device__ __forceinline__ SadBand sad_band_of(const SadRec& e, int x0, int y0, 
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// wave_shr:1 -- lane l receives lane l-1's value (lane 0: 0 by bound_ctrl;
-// no `old` operand, so no zeroing move per shift)
-__device__ __forceinline__ float shr1(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
-}
 
 // The 25-tap sums run as a systolic chain across lanes (round 2's two-phase
 // form staged the AD plane in LDS per wave and re-read it per tap: 3.35 ms
@@ -453,6 +448,8 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
       // B'. systolic: column 0 starts the chains (first tap: ((0+30)-30)+a = a
       // exactly), columns 1..4 continue the left neighbour's partials
       f32x2 p[TH];
+      float c30;  // 30.0f in a VGPR: the DPP add's second source
+      asm volatile("v_mov_b32 %0, 0x41f00000" : "=v"(c30));
 #pragma unroll
       for (int o = 0; o < TH; o++) {
         p[o] = ad[o];
@@ -460,15 +457,38 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
         for (int jj = 1; jj < 5; jj++) p[o] = ((p[o] + k30) - k30) + ad[o + jj];
       }
 #pragma unroll
-      for (int i = 1; i < 5; i++)
+      for (int i = 1; i < 5; i++) {
+        // the shift folded into the first add of the column: v_add_f32 with a
+        // DPP wave_shr:1 source (lane 0 reads 0 by bound_ctrl: 0 + 30), four
+        // rows per asm block.  The block's leading s_nop 1 gives the two wait
+        // states a DPP read of a VALU result needs (the compiler does not see
+        // inside inline asm); the pk ops below still pair the results.
+        float sx[TH], sy[TH];
+#pragma unroll
+        for (int o = 0; o < TH; o += 4)
+          asm volatile(
+              "s_nop 1\n\t"
+              "v_add_f32_dpp %0, %8, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "v_add_f32_dpp %1, %9, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "v_add_f32_dpp %2, %10, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "v_add_f32_dpp %3, %11, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "v_add_f32_dpp %4, %12, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "v_add_f32_dpp %5, %13, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "v_add_f32_dpp %6, %14, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "v_add_f32_dpp %7, %15, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+              : "=&v"(sx[o]), "=&v"(sy[o]), "=&v"(sx[o + 1]), "=&v"(sy[o + 1]), "=&v"(sx[o + 2]), "=&v"(sy[o + 2]),
+                "=&v"(sx[o + 3]), "=&v"(sy[o + 3])
+              : "v"(p[o].x), "v"(p[o].y), "v"(p[o + 1].x), "v"(p[o + 1].y), "v"(p[o + 2].x), "v"(p[o + 2].y),
+                "v"(p[o + 3].x), "v"(p[o + 3].y), "v"(c30));
 #pragma unroll
         for (int o = 0; o < TH; o++) {
-          f32x2 v = f32x2{shr1(p[o].x) + 30.0f, shr1(p[o].y) + 30.0f};
+          f32x2 v = f32x2{sx[o], sy[o]};
           v = (v - k30) + ad[o];
 #pragma unroll
           for (int jj = 1; jj < 5; jj++) v = ((v + k30) - k30) + ad[o + jj];
           p[o] = v;
         }
+      }
 #pragma unroll
       for (int o = 0; o < TH; o++) {
         mn[q][o].x = fminf(mn[q][o].x, p[o].x);

@@ -20,7 +20,8 @@ ranks come from the environment; `--gpus N` without WORLD_SIZE spawns the N
 rank processes itself before anything touches a GPU.  Every rank owns its own
 5-view stack (independent objects, no data-path collective) -> weak scaling;
 `view_sharded` adds C4 (one 32-view array sharded by reference view over the
-N GPUs, RCCL all-gathers) -> strong scaling.  Rank 0 prints ONE JSON line.
+N GPUs, RCCL all-gathers, the filter sharded by rows with a point-to-point
+rows -> views exchange) -> strong scaling.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 

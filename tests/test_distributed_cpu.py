@@ -81,7 +81,8 @@ def _worker(rank, world, port, name, outdir, bands=None, shard=None):
 # shard: the filter's sharding ("rows", the default, or "views"); bands: row
 # bands of the "views" form's pipelined proj all-gather (None: 2 at world > 1)
 @pytest.mark.parametrize("name,world,bands,shard", [("c3x1_s8", 2, None, "rows"), ("c3x1_s8", 3, None, "rows"),
-                                                    ("c2x2_s12", 2, None, "rows"), ("c3x1_s8", 2, None, "views"),
+                                                    ("c2x2_s12", 2, None, "rows"), ("c2x2_s12", 3, None, "rows"),
+                                                    ("c3x1_s8", 2, None, "views"),
                                                     ("c3x1_s8", 3, None, "views"), ("c2x2_s12", 2, 1, "views"),
                                                     ("c3x1_s8", 1, None, "rows"), ("c3x1_s8", 1, 3, "views")])
 def test_sharded_equals_unsharded(name, world, bands, shard):

@@ -33,6 +33,15 @@ __device__ __forceinline__ float round_ha(float v) {
   return truncf(v + copysignf(__int_as_float(0x3effffff), v));
 }
 
+// c - round_ha(v) as an int, for integral c: (int)(fc - round_ha(v)) without
+// the float subtract and truncate.  Equal wherever either lands in an image
+// ([0, 2^24)): round_ha(v) is then integral and exact, and outside it both are
+// out of range (the convert saturates; NaN converts to 0 either way, and a NaN
+// candidate votes 0 wherever it reads).
+__device__ __forceinline__ int sub_round_ha(int c, float v) {
+  return (int)((unsigned)c - (unsigned)(int)(v + copysignf(__int_as_float(0x3effffff), v)));
+}
+
 __device__ __forceinline__ float plane_at(float nx, float ny, float nz, float cx, float cy, float d, float px,
                                           float py) {
   float t = nx * (cx - px);
@@ -1275,12 +1284,12 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
       const bool live = k[s] < best;
       if (ROWB) {
         const float2 o = s_off[wave][j[s]];
-        const int yy = (int)(yf - round_ha(bd[s] * o.y));
+        const int yy = sub_round_ha(y, bd[s] * o.y);
         const bool yok = live && (unsigned)yy < (unsigned)H;
         const unsigned ro = jo[s] + __umul24((unsigned)yy, (unsigned)W) * 4u;
 #pragma unroll
         for (int u = 0; u < FB; u++) {
-          const int xx = (int)(xf - round_ha(d[s] * (o.x + (float)u)));
+          const int xx = sub_round_ha(x, d[s] * (u == 0 ? o.x : o.x + (float)u));  // dx integral: + 0 is exact
           in[s][u] = yok && j[s] + u < V && (unsigned)xx < (unsigned)W;
           // every lane issues its load (a skipped tap reads 0 past the buffer),
           // so the pass's gathers are in flight together
@@ -1291,8 +1300,8 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
 #pragma unroll
         for (int u = 0; u < FB; u++) {
           const float2 o = s_off[wave][min(j[s] + u, V - 1)];
-          const int xx = (int)(xf - round_ha(d[s] * o.x));
-          const int yy = (int)(yf - round_ha(bd[s] * o.y));
+          const int xx = sub_round_ha(x, d[s] * o.x);
+          const int yy = sub_round_ha(y, bd[s] * o.y);
           in[s][u] = live && j[s] + u < V && (unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H;
           const int off =
               in[s][u] ? (int)(jo[s] + (unsigned)u * P4 + (__umul24((unsigned)yy, (unsigned)W) + (unsigned)xx) * 4u) : 0x7fffffff;

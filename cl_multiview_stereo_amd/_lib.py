@@ -21,6 +21,7 @@ EXPORTS = [
     "mvs_box_stats_range_d", "mvs_set_ncc_variant", "mvs_ncc_last_variant", "mvs_init_state_range_d",
     "mvs_proj_inv_d", "mvs_remove_inconsistency_d", "mvs_proj_inv_rows_d", "mvs_remove_inconsistency_rows_d",
     "mvs_do_super_pixel_seg", "mvs_do_initial_depth_estimation", "mvs_do_refinement", "mvs_do_consistency_filter",
+    "mvs_init_state_range_l16_d", "mvs_propagate_l16_d", "mvs_spixl_to_image_l16_d",
 ]
 
 

@@ -153,7 +153,7 @@ void* scratch(mvs_ctx* ctx, size_t bytes, int* rc) {
 extern "C" {
 
 const char* mvs_last_error(void) { return g_err.c_str(); }
-const char* mvs_version(void) { return "mvs-mi355x 0.4 (gfx950)"; }
+const char* mvs_version(void) { return "mvs-mi355x 0.5 (gfx950)"; }
 
 int mvs_create(int device, mvs_ctx** out) {
   if (!out) return mvs::arg_fail("mvs_create: out is null");
@@ -360,39 +360,83 @@ int mvs_init_state_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const 
   if (!c || !spixl || !labels || !rep || !flat || !state || S <= 0 || bad_dims(W, H))
     return mvs::arg_fail("mvs_init_state_d: bad arguments");
   RC(upload_meta(c, a));
-  return mvs::launch_init_state(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, rep,
-                                flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state, 0,
+  return mvs::launch_init_state(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, 32,
+                                rep, flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state, 0,
                                 a->view_count);
+}
+
+// The refinement / fusion entry points over uint32 labels (lbits 32) or the
+// 16-bit maps of a narrowed all-gather (lbits 16: every label < mw * mh must
+// fit, so mw * mh <= 2^16 is required).
+static int labels_ok(int lbits, int W, int H, int S) {
+  return lbits == 32 || (lbits == 16 && (long)mvs::map_dim(W, S) * mvs::map_dim(H, S) <= (1L << 16));
+}
+
+static int init_state_range(mvs_ctx* c, int W, int H, int S, const float* spixl, const void* labels, int lbits,
+                            const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
+                            int kernel_steps, float kss, float fuse, int z0, int z1, float* state, const char* fn) {
+  if (!c || !spixl || !labels || !rep || !flat || !state || S <= 0 || bad_dims(W, H) || !labels_ok(lbits, W, H, S))
+    return mvs::arg_fail((std::string(fn) + ": bad arguments").c_str());
+  RC(upload_meta(c, a));
+  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail((std::string(fn) + ": bad view range").c_str());
+  return mvs::launch_init_state(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, lbits,
+                                rep, flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state, z0, z1);
 }
 
 int mvs_init_state_range_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels,
                            const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
                            int kernel_steps, float kss, float fuse, int z0, int z1, float* state) {
-  if (!c || !spixl || !labels || !rep || !flat || !state || S <= 0 || bad_dims(W, H))
-    return mvs::arg_fail("mvs_init_state_range_d: bad arguments");
+  return init_state_range(c, W, H, S, spixl, labels, 32, rep, flat, a, gamma, alpha, kernel_steps, kss, fuse, z0, z1,
+                          state, "mvs_init_state_range_d");
+}
+
+int mvs_init_state_range_l16_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint16_t* labels,
+                               const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
+                               int kernel_steps, float kss, float fuse, int z0, int z1, float* state) {
+  return init_state_range(c, W, H, S, spixl, labels, 16, rep, flat, a, gamma, alpha, kernel_steps, kss, fuse, z0, z1,
+                          state, "mvs_init_state_range_l16_d");
+}
+
+static int propagate(mvs_ctx* c, int W, int H, int S, const float* spixl, const void* labels, int lbits,
+                     const uint8_t* rep, const float* flat, const mvs_array* a, int iter, float alpha, float gamma,
+                     float fuse, int kernel_steps, float kss, const float* st_in, float* st_out, int z0, int z1,
+                     const char* fn) {
+  if (!c || !spixl || !labels || !rep || !flat || !st_in || !st_out || S <= 0 || bad_dims(W, H) ||
+      !labels_ok(lbits, W, H, S))
+    return mvs::arg_fail((std::string(fn) + ": bad arguments").c_str());
   RC(upload_meta(c, a));
-  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_init_state_range_d: bad view range");
-  return mvs::launch_init_state(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, rep,
-                                flat, c->d_vs, c->d_sn, gamma, alpha, kernel_steps, kss, fuse, state, z0, z1);
+  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail((std::string(fn) + ": bad view range").c_str());
+  return mvs::launch_propagate(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, lbits,
+                               rep, flat, c->d_vs, c->d_sn, iter, alpha, gamma, fuse, kernel_steps, kss, st_in,
+                               st_out, z0, z1);
 }
 
 int mvs_propagate_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels, const uint8_t* rep,
                     const float* flat, const mvs_array* a, int iter, float alpha, float gamma, float fuse,
                     int kernel_steps, float kss, const float* st_in, float* st_out, int z0, int z1) {
-  if (!c || !spixl || !labels || !rep || !flat || !st_in || !st_out || S <= 0 || bad_dims(W, H))
-    return mvs::arg_fail("mvs_propagate_d: bad arguments");
-  RC(upload_meta(c, a));
-  if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail("mvs_propagate_d: bad view range");
-  return mvs::launch_propagate(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, rep,
-                               flat, c->d_vs, c->d_sn, iter, alpha, gamma, fuse, kernel_steps, kss, st_in, st_out,
-                               z0, z1);
+  return propagate(c, W, H, S, spixl, labels, 32, rep, flat, a, iter, alpha, gamma, fuse, kernel_steps, kss, st_in,
+                   st_out, z0, z1, "mvs_propagate_d");
+}
+
+int mvs_propagate_l16_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint16_t* labels,
+                        const uint8_t* rep, const float* flat, const mvs_array* a, int iter, float alpha, float gamma,
+                        float fuse, int kernel_steps, float kss, const float* st_in, float* st_out, int z0, int z1) {
+  return propagate(c, W, H, S, spixl, labels, 16, rep, flat, a, iter, alpha, gamma, fuse, kernel_steps, kss, st_in,
+                   st_out, z0, z1, "mvs_propagate_l16_d");
 }
 
 int mvs_spixl_to_image_d(mvs_ctx* c, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
                          const float* state, float* disp) {
   if (!c || !spixl || !labels || !state || !disp || V <= 0 || S <= 0 || bad_dims(W, H))
     return mvs::arg_fail("mvs_spixl_to_image_d: bad arguments");
-  return mvs::launch_spixl_to_image(c->stream, V, W, H, S, spixl, labels, state, disp);
+  return mvs::launch_spixl_to_image(c->stream, V, W, H, S, spixl, labels, 32, state, disp);
+}
+
+int mvs_spixl_to_image_l16_d(mvs_ctx* c, int V, int W, int H, int S, const float* spixl, const uint16_t* labels,
+                             const float* state, float* disp) {
+  if (!c || !spixl || !labels || !state || !disp || V <= 0 || S <= 0 || bad_dims(W, H) || !labels_ok(16, W, H, S))
+    return mvs::arg_fail("mvs_spixl_to_image_l16_d: bad arguments");
+  return mvs::launch_spixl_to_image(c->stream, V, W, H, S, spixl, labels, 16, state, disp);
 }
 
 // clDepthRefinement::do_refinement + fusion (depth_refinement.cpp:91-118, 1318-1370)

@@ -96,16 +96,17 @@ int launch_wta(hipStream_t s, int W, int H, int D, const float* vol, const float
                float* conf);
 
 int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, float gamma, float* flat);
+// labels: uint32, or uint16 when lbits == 16 (16-bit gathered maps)
 int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
-                      const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                      const void* labels, int lbits, const uint8_t* rep, const float* flat, const int* vs,
                       const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state,
                       int z0, int z1);
 int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
-                     const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                     const void* labels, int lbits, const uint8_t* rep, const float* flat, const int* vs,
                      const int* sn, int iter, float alpha, float gamma, float fuse, int nks, float kss,
                      const float* st_in, float* st_out, int z0, int z1);
 int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float* spixl,
-                          const uint32_t* labels, const float* state, float* disp);
+                          const void* labels, int lbits, const float* state, float* disp);
 int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,
                   float* proj, float* out, int z0, int z1);
 int launch_proj_inv(hipStream_t s, int V, int W, int H, int aw, float bl, const float* full, float* proj, int z0,

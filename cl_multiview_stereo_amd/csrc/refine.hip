@@ -138,7 +138,17 @@ __device__ __forceinline__ float finish_consistency(float cons, int vc) {
   return vc > 0 ? fmaxf(margin, cons / (float)vc) : margin;
 }
 
-__device__ float init_consistency(const RArgs& c, const float* __restrict__ spixl, const uint32_t* __restrict__ labels,
+// Label maps are uint32 (the reference's layout) or uint16 (LT): the
+// view-sharded pipeline all-gathers them as 16-bit values when every label
+// (< mw * mh <= 2^16) fits, and the refinement and fusion read them as they
+// arrive instead of after a widening pass.
+template <typename LT>
+__device__ __forceinline__ uint32_t label_at(const void* labels, long i) {
+  return ((const LT*)labels)[i];
+}
+
+template <typename LT>
+__device__ float init_consistency(const RArgs& c, const float* __restrict__ spixl, const void* __restrict__ labels,
                                   const uint8_t* rp, const int* __restrict__ vs, const int* __restrict__ sn, int z,
                                   const float* color, float cxf, float cyf, float d, float2 fl) {
   long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
@@ -164,7 +174,7 @@ __device__ float init_consistency(const RArgs& c, const float* __restrict__ spix
       const int xp = (int)((float)xr - roundf(d * (float)(vx - camx)));
       const int yp = (int)((float)yr - roundf((c.bl * d) * (float)(vy - camy)));
       okv[t] = xp >= 0 && yp >= 0 && xp < c.W && yp < c.H;
-      ipv[t] = labels[P * view + (okv[t] ? (long)c.W * yp + xp : 0)];
+      ipv[t] = label_at<LT>(labels, P * view + (okv[t] ? (long)c.W * yp + xp : 0));
     }
     float r3[9], r4[9], r5[9], r7[9];
 #pragma unroll
@@ -194,8 +204,9 @@ __device__ float init_consistency(const RArgs& c, const float* __restrict__ spix
   return finish_consistency(cons, vc);
 }
 
+template <typename LT>
 __global__ __launch_bounds__(256) void k_init_state(RArgs c, const float* __restrict__ spixl,
-                                                    const uint32_t* __restrict__ labels,
+                                                    const void* __restrict__ labels,
                                                     const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
                                                     const int* __restrict__ vs, const int* __restrict__ sn, int nks,
                                                     float kss, int z0, float* __restrict__ state) {
@@ -207,7 +218,7 @@ __global__ __launch_bounds__(256) void k_init_state(RArgs c, const float* __rest
   float2 fl = flat[idx];
   float sm = init_smoothness(c, spixl, sp, fl, x, y, z, nks, kss);
   float color[3] = {sp[3], sp[4], sp[5]};
-  float cs = init_consistency(c, spixl, labels, rep + 8 * idx, vs, sn, z, color, sp[1], sp[2], sp[7], fl);
+  float cs = init_consistency<LT>(c, spixl, labels, rep + 8 * idx, vs, sn, z, color, sp[1], sp[2], sp[7], fl);
   float* o = state + 6 * idx;
   o[0] = sp[7]; o[1] = sm; o[2] = cs; o[3] = 0.0f; o[4] = 0.0f; o[5] = 1.0f;
 }
@@ -220,7 +231,7 @@ struct PState {
 struct PCtx {
   RArgs c;
   const float* spixl;
-  const uint32_t* labels;
+  const void* labels;  // uint32 or uint16 (the reader's LT)
   const int* vs;
   const int* sn;
   const float* st;
@@ -278,6 +289,7 @@ __device__ float comp_smoothness(const PCtx& p, float d, float nx, float ny, flo
 // leaves every sum unchanged), so the gathers overlap instead of forming 9
 // round trips.  A label is the superpixel index y*mw + x, so the record is at
 // view * M + label (the reference's % and / recombine to it exactly).
+template <typename LT>
 __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, float nz) {
   const RArgs& c = p.c;
   const long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
@@ -296,7 +308,7 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
   for (int k = 0; k < p.sn[p.z]; k++) {
     const int view = p.vs[c.V * p.z + k];
     const float fdx = (float)(view % c.aw - camx), fdy = (float)(view / c.aw - camy);
-    const uint32_t* lv = p.labels + P * view;
+    const long lv = P * view;
     int xp[9], yp[9];
     bool ok[9];
     uint32_t ip[9];
@@ -305,7 +317,7 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
       xp[s] = (int)(sxf[s] - roundf(di[s] * fdx));
       yp[s] = (int)(syf[s] - roundf((c.bl * di[s]) * fdy));
       ok[s] = xp[s] >= 0 && yp[s] >= 0 && xp[s] < c.W && yp[s] < c.H;
-      ip[s] = lv[ok[s] ? (long)c.W * yp[s] + xp[s] : 0];
+      ip[s] = label_at<LT>(p.labels, lv + (ok[s] ? (long)c.W * yp[s] + xp[s] : 0));
     }
     float vis_w = 0.0f, occ_w = 0.0f, num = 0.0f, visibility = 0.0f, visible = 0.0f;
 #pragma unroll
@@ -353,6 +365,7 @@ __device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, fl
 // (t_vis, t_col) and (ok, wv) go to LDS, and view_sum adds a view's 9 samples
 // in order (each view's sums start at 0, as in the reference).  Same
 // arithmetic as comp_consistency, bit for bit.
+template <typename LT>
 __device__ __forceinline__ void view_tasks(const PCtx& p, int r, int L, int nv, const int2* toff,
                                            const float4* tview, const float* sdi, float2* samp, uint8_t* sflg) {
   const RArgs& c = p.c;
@@ -383,7 +396,7 @@ __device__ __forceinline__ void view_tasks(const PCtx& p, int r, int L, int nv, 
         xp[i] = (int)(sxf - round_ha(di[i] * tv.y));
         yp[i] = (int)(syf - round_ha((c.bl * di[i]) * tv.z));
         ok[i] = xp[i] >= 0 && yp[i] >= 0 && xp[i] < c.W && yp[i] < c.H;
-        ip[i] = p.labels[P * view + (ok[i] ? (long)c.W * yp[i] + xp[i] : 0)];
+        ip[i] = label_at<LT>(p.labels, P * view + (ok[i] ? (long)c.W * yp[i] + xp[i] : 0));
         vw[i] = view;
       }
     }
@@ -447,8 +460,9 @@ __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
+template <typename LT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_propagate(RArgs c, const float* __restrict__ spixl,
-                                                   const uint32_t* __restrict__ labels,
+                                                   const void* __restrict__ labels,
                                                    const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
                                                    const int* __restrict__ vs, const int* __restrict__ sn, int iter,
                                                    int nks, float kss, const float* __restrict__ st_in,
@@ -659,7 +673,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (ok) view_tasks(p, r, L, nv, s_toff[w], s_tview[w], s_di[w][t], s_samp[w][t], s_sflg[w][t]);
+      if (ok) view_tasks<LT>(p, r, L, nv, s_toff[w], s_tview[w], s_di[w][t], s_samp[w][t], s_sflg[w][t]);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -719,7 +733,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         t = t + nz * s1[0];
         di = t / nz;
         sm1 = smooth(di, nx, ny, nz);
-        cs1 = comp_consistency(p, di, nx, ny, nz);
+        cs1 = comp_consistency<LT>(p, di, nx, ny, nz);
         const float diff = mvs_distance3(p.col[0], p.col[1], p.col[2], sc[3], sc[4], sc[5]);
         simi = expf_neg_sq(diff, c.gamma);
       }
@@ -761,7 +775,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
           n0 = n0 / rr; n1 = n1 / rr; n2 = n2 / rr;
         }
         sm1 = smooth(cur.d, n0, n1, n2);
-        cs1 = comp_consistency(p, cur.d, n0, n1, n2);
+        cs1 = comp_consistency<LT>(p, cur.d, n0, n1, n2);
       }
       const unsigned long long valid = __ballot(ok);
       for (int l = 0; l < 8; l++) {
@@ -780,7 +794,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // ---- spixl_to_image ----------------------------------------------------------
-__global__ void k_spixl_to_image(const float* __restrict__ spixl, const uint32_t* __restrict__ labels,
+template <typename LT>
+__global__ void k_spixl_to_image(const float* __restrict__ spixl, const LT* __restrict__ labels,
                                  const float* __restrict__ st, int W, int H, int mw, int mh,
                                  float* __restrict__ disp) {
   int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
@@ -797,13 +812,14 @@ __global__ void k_spixl_to_image(const float* __restrict__ spixl, const uint32_t
   disp[P * z + (long)W * y + x] = v / t[5];
 }
 
-// The same map, 4 consecutive pixels per thread (W % 4 == 0): one 16-B label
-// load and one 16-B store per thread, the record gathers as buffer loads
+// The same map, 4 consecutive pixels per thread (W % 4 == 0): one 16-B (u32
+// labels) or 8-B (u16) label load and one 16-B store per thread, the record gathers as buffer loads
 // with 32-bit offsets inside view z's records (a label is the superpixel
 // index sy * mw + sx, so the record is at M * z + label, as in
 // comp_consistency).  Same arithmetic per pixel.
+template <typename LT>
 __global__ __launch_bounds__(256) void k_spixl_to_image4(const float* __restrict__ spixl,
-                                                         const uint32_t* __restrict__ labels,
+                                                         const LT* __restrict__ labels,
                                                          const float* __restrict__ st, int W, int H, int mw, int mh,
                                                          float* __restrict__ disp) {
   const int x = 4 * (blockIdx.x * blockDim.x + threadIdx.x), y = blockIdx.y, z = blockIdx.z;
@@ -811,8 +827,14 @@ __global__ __launch_bounds__(256) void k_spixl_to_image4(const float* __restrict
   const long M = (long)mw * mh, P = (long)W * H, p = P * z + (long)W * y + x;
   const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc((void*)(spixl + 8 * M * z), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc((void*)(st + 6 * M * z), 0, 0x7fffffff, 0x00020000);
-  const uint4 id4 = *(const uint4*)(labels + p);
-  const unsigned ids[4] = {id4.x, id4.y, id4.z, id4.w};
+  unsigned ids[4];
+  if (sizeof(LT) == 4) {
+    const uint4 id4 = *(const uint4*)(labels + p);
+    ids[0] = id4.x, ids[1] = id4.y, ids[2] = id4.z, ids[3] = id4.w;
+  } else {
+    const uint2 id4 = *(const uint2*)(labels + p);
+    ids[0] = id4.x & 0xffffu, ids[1] = id4.x >> 16, ids[2] = id4.y & 0xffffu, ids[3] = id4.y >> 16;
+  }
   float s1[4], s2[4], t0[4], t3[4], t4[4], t5[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -1349,39 +1371,50 @@ int launch_flatness(hipStream_t s, int V, int mw, int mh, const float* spixl, fl
 }
 
 int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
-                      const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                      const void* labels, int lbits, const uint8_t* rep, const float* flat, const int* vs,
                       const int* sn, float gamma, float alpha, int nks, float kss, float fuse, float* state,
                       int z0, int z1) {
   if (z1 <= z0) return 0;
   RArgs c{V, W, H, S, map_dim(W, S), map_dim(H, S), aw, bl, fuse, alpha, gamma};
-  hipLaunchKernelGGL(k_init_state, dim3((c.mw + 63) / 64, c.mh, z1 - z0), dim3(64), 0, s, c, spixl, labels, rep,
+  hipLaunchKernelGGL(lbits == 16 ? k_init_state<uint16_t> : k_init_state<uint32_t>, dim3((c.mw + 63) / 64, c.mh, z1 - z0), dim3(64), 0, s, c, spixl, labels, rep,
                      (const float2*)flat, vs, sn, nks, kss, z0, state);
   MVS_LAUNCH_CHECK("k_init_state");
   return 0;
 }
 
 int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
-                     const uint32_t* labels, const uint8_t* rep, const float* flat, const int* vs,
+                     const void* labels, int lbits, const uint8_t* rep, const float* flat, const int* vs,
                      const int* sn, int iter, float alpha, float gamma, float fuse, int nks, float kss,
                      const float* st_in, float* st_out, int z0, int z1) {
   if (z1 <= z0) return 0;
   RArgs c{V, W, H, S, map_dim(W, S), map_dim(H, S), aw, bl, fuse, alpha, gamma};
   const long nsp = (long)c.mw * c.mh * (z1 - z0);
-  hipLaunchKernelGGL(k_propagate, dim3((unsigned)((nsp + 3) / 4)), dim3(256), 0, s, c, spixl, labels, rep,
+  hipLaunchKernelGGL(lbits == 16 ? k_propagate<uint16_t> : k_propagate<uint32_t>, dim3((unsigned)((nsp + 3) / 4)), dim3(256), 0, s, c, spixl, labels, rep,
                      (const float2*)flat, vs, sn, iter, nks, kss, st_in, st_out, z0, nsp);
   MVS_LAUNCH_CHECK("k_propagate");
   return 0;
 }
 
-int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
-                          const float* state, float* disp) {
+int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float* spixl, const void* labels,
+                          int lbits, const float* state, float* disp) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
-  // the 4-pixel form needs 16-B aligned rows and 32-bit record offsets
-  if (W % 4 == 0 && (long)mw * mh * 32 < (1L << 31) && ((uintptr_t)labels & 15) == 0 && ((uintptr_t)disp & 15) == 0)
-    hipLaunchKernelGGL(k_spixl_to_image4, dim3((W / 4 + 255) / 256, H, V), dim3(256), 0, s, spixl, labels, state, W,
-                       H, mw, mh, disp);
+  // the 4-pixel form needs aligned 4-label loads, 16-B aligned stores and
+  // 32-bit record offsets
+  const bool l16 = lbits == 16;
+  const uintptr_t la = (uintptr_t)labels & (l16 ? 7 : 15);
+  const bool four = W % 4 == 0 && (long)mw * mh * 32 < (1L << 31) && la == 0 && ((uintptr_t)disp & 15) == 0;
+  const dim3 g4((W / 4 + 255) / 256, H, V), g1((W + 255) / 256, H, V);
+  if (four && l16)
+    hipLaunchKernelGGL(k_spixl_to_image4<uint16_t>, g4, dim3(256), 0, s, spixl, (const uint16_t*)labels, state, W, H,
+                       mw, mh, disp);
+  else if (four)
+    hipLaunchKernelGGL(k_spixl_to_image4<uint32_t>, g4, dim3(256), 0, s, spixl, (const uint32_t*)labels, state, W, H,
+                       mw, mh, disp);
+  else if (l16)
+    hipLaunchKernelGGL(k_spixl_to_image<uint16_t>, g1, dim3(256), 0, s, spixl, (const uint16_t*)labels, state, W, H,
+                       mw, mh, disp);
   else
-    hipLaunchKernelGGL(k_spixl_to_image, dim3((W + 255) / 256, H, V), dim3(256), 0, s, spixl, labels, state, W, H,
+    hipLaunchKernelGGL(k_spixl_to_image<uint32_t>, g1, dim3(256), 0, s, spixl, (const uint32_t*)labels, state, W, H,
                        mw, mh, disp);
   MVS_LAUNCH_CHECK("k_spixl_to_image");
   return 0;

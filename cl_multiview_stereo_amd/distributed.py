@@ -212,11 +212,15 @@ class ShardOutput:
     z0: int
     z1: int
     spixl: torch.Tensor                 # [V, mh, mw, 8] (gathered, s7 = seed disparity)
-    labels: torch.Tensor                # [V, H, W]      (gathered)
+    labels: torch.Tensor                # [V, H, W]      (gathered; int32, or uint16 after a narrowed gather)
     disp: torch.Tensor | None = None    # [z1-z0, H, W] per-pixel NCC/SAD disparity
     conf: torch.Tensor | None = None
     disp_refined: torch.Tensor | None = None   # [z1-z0, H, W]
     disp_filtered: torch.Tensor | None = None  # [z1-z0, H, W]
+
+    def labels32(self) -> torch.Tensor:
+        """The gathered labels as int32 (uint32 bits), widening 16-bit maps."""
+        return self.labels if self.labels.dtype == torch.int32 else self.labels.to(torch.int32)
 
 
 class ShardedPipeline:
@@ -254,7 +258,8 @@ class ShardedPipeline:
         # the labels (the largest gather) are read from other views only by the
         # refinement: in flight while this rank sweeps its block.  With fewer
         # than 2^16 superpixels per view they travel as 16-bit values (half the
-        # bytes over xGMI), widened after the wait.
+        # bytes over xGMI), and the refinement and fusion kernels
+        # read them as they arrive (no widening pass).
         narrow = _narrow_labels(g, spixl)
         if narrow:
             l16 = torch.empty(labels.shape, dtype=torch.int16, device=labels.device)
@@ -270,7 +275,7 @@ class ShardedPipeline:
         out.spixl = g(spixl[z0:z1], spixl)  # centres + seeds (s7) of every view
         if narrow:
             pending.wait()
-            out.labels = l16.view(torch.uint16).to(torch.int32)  # one widening pass
+            out.labels = l16.view(torch.uint16)
         else:
             out.labels = pending.wait()
         spixl, labels = out.spixl, out.labels

@@ -5,7 +5,8 @@ compute step is a hand-written HIP kernel reached through the C-ABI in
 include/mvs.h.  Tensors are in the reference layouts:
 
     rgbx   uint8   [V, H, W, 4]     lab    float32 [V, H, W, 4]
-    spixl  float32 [V, mh, mw, 8]   labels int32   [V, H, W] (uint32 bits)
+    spixl  float32 [V, mh, mw, 8]   labels int32   [V, H, W] (uint32 bits; the refinement
+                                    and fusion also take 16-bit maps)
     rep    uint8   [V, mh, mw, 8]   state  float32 [V, mh, mw, 6]
     disp   float32 [V, H, W]
 """
@@ -29,6 +30,16 @@ def _ptr(t: torch.Tensor | None):
     if not t.is_contiguous():
         raise ValueError("tensor must be contiguous")
     return C.c_void_p(t.data_ptr())
+
+
+def _label_fn(L, name: str, labels: torch.Tensor):
+    """The uint32 entry point `name`_d, or its 16-bit twin `name`_l16_d for
+    int16/uint16 label maps (the narrowed all-gather's; bits read unsigned)."""
+    if labels.dtype == torch.int32:
+        return getattr(L, name + "_d")
+    if labels.dtype in (torch.int16, torch.uint16):
+        return getattr(L, name + "_l16_d")
+    raise ValueError(f"labels must be int32 or 16-bit, not {labels.dtype}")
 
 
 def _runs(views):
@@ -312,15 +323,17 @@ class Engine:
 
     def init_state_range(self, spixl, labels, rep, flat, cam: CameraArray, S, gamma, alpha, nks, kss, fuse, z0, z1,
                          state=None):
-        """init_current_state for views [z0, z1) into a full [V, mh, mw, 6] state."""
+        """init_current_state for views [z0, z1) into a full [V, mh, mw, 6] state.
+        labels: int32, or int16/uint16 (16-bit maps, mw * mh <= 65536)."""
         V, H, W = labels.shape
         mw, mh = map_size(W, H, S)
         st = self.empty((V, mh, mw, 6), torch.float32) if state is None else state
         self._stream()
-        _lib.check(self.L.mvs_init_state_range_d(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), _ptr(flat),
+        fn = _label_fn(self.L, "mvs_init_state_range", labels)
+        _lib.check(fn(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), _ptr(flat),
                                                  cam.desc(), C.c_float(gamma), C.c_float(alpha), int(nks),
                                                  C.c_float(kss), C.c_float(fuse), int(z0), int(z1), _ptr(st)),
-                   "mvs_init_state_range_d")
+                   fn.__name__)
         return st
 
     def propagate(self, spixl, labels, rep, flat, cam: CameraArray, S, it, alpha, gamma, fuse, nks, kss, st_in,
@@ -328,18 +341,19 @@ class Engine:
         V, H, W = labels.shape
         z1 = V if z1 is None else z1
         self._stream()
-        _lib.check(self.L.mvs_propagate_d(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), _ptr(flat),
+        fn = _label_fn(self.L, "mvs_propagate", labels)
+        _lib.check(fn(self.ctx, W, H, S, _ptr(spixl), _ptr(labels), _ptr(rep), _ptr(flat),
                                           cam.desc(), int(it), C.c_float(alpha), C.c_float(gamma), C.c_float(fuse),
                                           int(nks), C.c_float(kss), _ptr(st_in), _ptr(st_out), int(z0), int(z1)),
-                   "mvs_propagate_d")
+                   fn.__name__)
         return st_out
 
     def spixl_to_image(self, spixl, labels, state, S):
         V, H, W = labels.shape
         disp = self.empty((V, H, W), torch.float32)
         self._stream()
-        _lib.check(self.L.mvs_spixl_to_image_d(self.ctx, V, W, H, S, _ptr(spixl), _ptr(labels), _ptr(state),
-                                               _ptr(disp)), "mvs_spixl_to_image_d")
+        fn = _label_fn(self.L, "mvs_spixl_to_image", labels)
+        _lib.check(fn(self.ctx, V, W, H, S, _ptr(spixl), _ptr(labels), _ptr(state), _ptr(disp)), fn.__name__)
         return disp
 
     def filter(self, disp_full, array_width: int, bl_ratio: float, fuse: float = 1.0, z0: int = 0, z1=None,

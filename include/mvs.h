@@ -203,6 +203,19 @@ int mvs_propagate_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const
                     int z0, int z1);
 int mvs_spixl_to_image_d(mvs_ctx* ctx, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,
                          const float* state, float* disp);
+/* ABI 0.5: the same three passes over 16-bit label maps (uint16 [V][H][W], the
+ * view-sharded pipeline's narrowed labels all-gather; requires
+ * mw * mh <= 65536, else MVS_E_ARG).  Results are identical to the uint32
+ * entry points on the same label values. */
+int mvs_init_state_range_l16_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint16_t* labels,
+                               const uint8_t* rep, const float* flat, const mvs_array* a, float gamma, float alpha,
+                               int kernel_steps, float kss, float fuse, int z0, int z1, float* state);
+int mvs_propagate_l16_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint16_t* labels,
+                        const uint8_t* rep, const float* flat, const mvs_array* a, int iter, float alpha,
+                        float gamma, float fuse, int kernel_steps, float kss, const float* st_in, float* st_out,
+                        int z0, int z1);
+int mvs_spixl_to_image_l16_d(mvs_ctx* ctx, int V, int W, int H, int S, const float* spixl, const uint16_t* labels,
+                             const float* state, float* disp);
 int mvs_refine_d(mvs_ctx* ctx, int W, int H, int S, const float* spixl, const uint32_t* labels,
                  const uint8_t* rep, const mvs_array* a, const mvs_refine_params* p, float* flat,
                  float* state, float* state2, float* disp);

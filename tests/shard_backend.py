@@ -14,6 +14,12 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
+def _lab(t):
+    """Label maps as uint32: int32 bits, or 16-bit maps (the narrowed gather) widened."""
+    a = _np(t)
+    return a.view(np.uint32) if a.dtype.itemsize == 4 else a.view(np.uint16).astype(np.uint32)
+
+
 class OracleBackend:
     def cvt(self, rgbx, views):
         # only the listed views are converted; the rest stay NaN / 0xff so a
@@ -35,7 +41,7 @@ class OracleBackend:
 
     def boundary(self, spixl, labels, S, z0, z1):
         rep = np.full(tuple(spixl.shape[:3]) + (8,), 255, np.uint8)
-        rep[z0:z1] = orc.boundary(_np(spixl)[z0:z1], _np(labels).view(np.uint32)[z0:z1], S)
+        rep[z0:z1] = orc.boundary(_np(spixl)[z0:z1], _lab(labels)[z0:z1], S)
         return torch.from_numpy(rep)
 
     def sweep_spixl(self, lab, spixl, rep, cam, S, z0, z1):
@@ -63,21 +69,21 @@ class OracleBackend:
     def init_state(self, spixl, labels, rep, flat, cam, S, gamma, alpha, nks, kss, fuse, z0, z1):
         r = np.zeros_like(_np(rep))  # the oracle runs every view: give the others harmless extents
         r[z0:z1] = _np(rep)[z0:z1]
-        st = orc.init_state(_np(spixl), _np(labels).view(np.uint32), r, _np(flat), cam.view_subset,
+        st = orc.init_state(_np(spixl), _lab(labels), r, _np(flat), cam.view_subset,
                             cam.subset_num, cam.array_width, cam.bl_ratio, S, gamma, alpha, nks, kss, fuse)
         out = np.full(st.shape, np.nan, np.float32)
         out[z0:z1] = st[z0:z1]
         return torch.from_numpy(out)
 
     def propagate(self, spixl, labels, rep, flat, cam, S, it, alpha, gamma, fuse, nks, kss, st_in, st_out, z0, z1):
-        out = orc.propagate(_np(spixl), _np(labels).view(np.uint32), _np(rep), _np(flat), cam.view_subset,
+        out = orc.propagate(_np(spixl), _lab(labels), _np(rep), _np(flat), cam.view_subset,
                             cam.subset_num, cam.array_width, cam.bl_ratio, S, it, alpha, gamma, fuse, nks, kss,
                             _np(st_in), z0, z1)
         st_out[z0:z1] = torch.from_numpy(out[z0:z1])
         return st_out
 
     def spixl_to_image(self, spixl, labels, state, S):
-        return torch.from_numpy(orc.spixl_to_image(_np(spixl), _np(labels).view(np.uint32), _np(state), S))
+        return torch.from_numpy(orc.spixl_to_image(_np(spixl), _lab(labels), _np(state), S))
 
     def proj_inv(self, disp_full, aw, bl, z0, z1, proj=None, rows=None, band=False):
         oproj, _ = orc.filt(_np(disp_full), aw, bl, 1.0)

@@ -72,7 +72,7 @@ def _worker(rank, world, port, name, outdir, bands=None, shard=None):
                                filter_shard=shard)
         out = pipe.run(torch.from_numpy(b["stack"]))
         np.savez(os.path.join(outdir, f"r{rank}.npz"), z=np.array([out.z0, out.z1]), spixl=out.spixl.numpy(),
-                 labels=out.labels.numpy().view(np.uint32), disp=out.disp.numpy(),
+                 labels=out.labels32().numpy().view(np.uint32), disp=out.disp.numpy(),
                  refined=out.disp_refined.numpy(), filt=out.disp_filtered.numpy())
     finally:
         dist.destroy_process_group()

@@ -43,7 +43,7 @@ def _worker(rank, world, port, name, outdir, bands, shard):
         out = pipe.run(torch.from_numpy(b["stack"]).cuda())
         torch.cuda.synchronize()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), z=np.array([out.z0, out.z1]), spixl=out.spixl.cpu().numpy(),
-                 labels=out.labels.cpu().numpy().view(np.uint32), disp=out.disp.cpu().numpy(),
+                 labels=out.labels32().cpu().numpy().view(np.uint32), disp=out.disp.cpu().numpy(),
                  refined=out.disp_refined.cpu().numpy(), filt=out.disp_filtered.cpu().numpy())
     finally:
         dist.destroy_process_group()

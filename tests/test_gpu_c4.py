@@ -67,7 +67,7 @@ def _bits(t):
 
 def _check(out, want, z0, z1):
     """Gathered labels / spixl of every view, and the rank's own block of maps."""
-    assert np.array_equal(_bits(out.labels), want["labels"]), "labels"
+    assert np.array_equal(_bits(out.labels32()), want["labels"]), "labels"
     assert np.array_equal(_bits(out.spixl), want["spixl"].view(np.uint32)), "spixl (centres + seeds)"
     for k, t in (("disp", out.disp), ("refined", out.disp_refined), ("filt", out.disp_filtered)):
         assert np.array_equal(_bits(t), want[k][z0:z1].view(np.uint32)), k

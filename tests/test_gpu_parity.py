@@ -284,6 +284,65 @@ def test_refinement(engine, name, ks, kst):
         cur = nxt
 
 
+def _refine_stages(engine, sp, lb, rep, cam, S, ks=1080, kst=13):
+    """init state, the 5 propagate iterations and the fused map, with the
+    refinement's parameters: the entry points chosen by the labels' dtype."""
+    V = lb.shape[0]
+    rp = params.refine_params(params.Settings(spixl_size=S, kernel_size=ks, kernel_step=kst))
+    flat = engine.flatness(sp, rp["flat_gamma"])
+    cur = engine.init_state_range(sp, lb, rep, flat, cam, S, rp["init_gamma"], rp["init_alpha"], rp["kernel_steps"],
+                                  rp["kss"], rp["fuse"], 0, V)
+    out = [cur.clone()]
+    for it in range(5):
+        nks, kss = params.prop_schedule(it, rp["kernel_steps"], rp["kss"])
+        nxt = torch.empty_like(cur)
+        engine.propagate(sp, lb, rep, flat, cam, S, it, rp["prop_alpha"], rp["prop_gamma"], rp["fuse"], nks, kss,
+                         cur, nxt)
+        out.append(nxt)
+        cur = nxt
+    out.append(engine.spixl_to_image(sp, lb, cur, S))
+    return [t.cpu().numpy() for t in out]
+
+
+@pytest.mark.parametrize("name", ["c3x3_s8", "c5x1_s32"])
+def test_refinement_labels16(engine, name):
+    """The 16-bit label entry points (the sharded pipeline's narrowed labels,
+    ABI 0.5) against the oracle, stage by stage."""
+    c = CASES[name]
+    b = build(c)
+    lab, sp, lb, rep = _chain(engine, c, b)
+    cam = CameraArray(c["aw"], c["bl"], b["levels"], b["vs"], b["sn"])
+    engine.sweep_spixl(lab, sp, rep, cam, c["S"])
+    want = orc.refine(sp.cpu().numpy(), as_u32(lb), rep.cpu().numpy(), b["vs"], b["sn"], c["aw"], c["bl"], c["S"],
+                      2.0, 6.0, 1.0, 13, 1080, 5, True)
+    got = _refine_stages(engine, sp, lb.to(torch.int16).view(torch.uint16), rep, cam, c["S"])
+    assert_bits(got[0], want["state0"], "init state (16-bit labels)")
+    for it in range(5):
+        assert_bits(got[1 + it], want["states"][it], f"propagate iteration {it} (16-bit labels)")
+
+
+@pytest.mark.parametrize("W", [400, 398])  # 398: the one-pixel fusion kernel (W % 4 != 0)
+def test_labels16_above_32767(engine, W):
+    """Labels with the top bit of 16 set (S = 2: 40,000 superpixels per view)
+    read unsigned: every stage equal to the uint32 entry points bit for bit."""
+    S = 2
+    stack, _ = synth.make_stack(W, 400, 3, 1, 0, 15, 1.0, 5)
+    vs, sn = params.flatten_subsets(params.neighbour_lists(3, 1, 1, 0))
+    cam = CameraArray(3, 1.0, params.disparity_levels(0, 15, 1), vs, sn)
+    lab, _ = engine.cvt(dev(stack))
+    sp, lb = engine.grid(lab, S)
+    rep = engine.boundary(sp, lb, S)
+    engine.sweep_spixl(lab, sp, rep, cam, S)
+    assert int(lb.max()) >= 1 << 15
+    want = _refine_stages(engine, sp, lb, rep, cam, S)
+    got = _refine_stages(engine, sp, lb.to(torch.int16).view(torch.uint16), rep, cam, S)
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert_bits(g, w, f"stage {k} (16-bit vs 32-bit labels)")
+    with pytest.raises(Exception, match="bad arguments"):  # 16-bit maps need mw * mh <= 65536
+        sp1, lb1 = engine.grid(lab, 1)
+        engine.spixl_to_image(sp1, lb1.to(torch.int16), torch.zeros(3, 400, W, 6, device="cuda"), 1)
+
+
 @pytest.mark.parametrize("name", ["c3x3_s8", "c3x1_s16"])
 def test_filter(engine, name):
     c = CASES[name]

@@ -32,7 +32,7 @@ def test_sharded_pipeline_world1(engine, name, fused, bands):
     pipe = ShardedPipeline(EngineBackend(engine, fused=fused), _settings(c), cam, ViewGather(b["V"]),
                            proj_bands=bands)
     out = pipe.run(torch.from_numpy(b["stack"]).cuda())
-    assert np.array_equal(bits(out.labels), want["labels"])
+    assert np.array_equal(bits(out.labels32()), want["labels"])
     assert np.array_equal(bits(out.spixl), want["spixl"].view(np.uint32))
     for k, t in (("disp", out.disp), ("refined", out.disp_refined), ("filt", out.disp_filtered)):
         assert np.array_equal(bits(t), want[k].view(np.uint32)), k

@@ -43,6 +43,7 @@ def main():
     nblk = int(os.environ.get("BLOCKS", "60"))
     cx, cy = np.arange(V) % aw, np.arange(V) // aw
     nat, srt, tot_g, pix = 0.0, 0.0, 0.0, 0
+    lanes = []
     for _ in range(nblk):
         y = int(rng.integers(0, H))
         xb = int(rng.integers(0, W // 256)) * 256
@@ -79,6 +80,7 @@ def main():
                     break
             work.append(g)
         work = np.array(work, float)
+        lanes.append(work)
         nds = np.array(nds)
         tot_g += work.sum()
         pix += 256
@@ -88,9 +90,27 @@ def main():
         srt += sum(ws[64 * w:64 * w + 64].max() for w in range(4))
         order2 = np.argsort(-work, kind="stable")  # oracle: sorted by the true work
         ws2 = work[order2]
+    # a capped first pass (each wave stops after K gathers per lane; lanes not
+    # done are queued) plus a second pass over the queue, packed 64 to a wave:
+    # wave cost per 64 pixels, in gathers, with `prep` gathers' worth of
+    # restart cost per queued pixel
+    allw = np.concatenate(lanes)
+    waves = allw.reshape(-1, 64)
+    split = {}
+    for K in (8, 12, 16, 20, 24, 32):
+        a_cost = np.minimum(waves.max(1), K).sum()
+        ex = allw[allw > K] - K
+        out = {}
+        for prep in (0, 4, 8):
+            q = rng.permutation(ex + prep)
+            q = np.concatenate([q, np.zeros((-len(q)) % 64)]).reshape(-1, 64)
+            out[f"prep{prep}"] = round(float((a_cost + q.max(1).sum()) / len(waves)), 2)
+        out["queued_frac"] = round(float(len(ex) / len(allw)), 3)
+        split[f"K{K}"] = out
+    pct = {f"p{q}": float(np.percentile(allw, q)) for q in (50, 75, 90, 95, 99)}
     print(json.dumps({"blocks": nblk, "mean_gathers_per_pixel": tot_g / pix,
                       "wave_cost_natural": nat / (4 * nblk), "wave_cost_sorted_by_nd": srt / (4 * nblk),
-                      "lane_mean": tot_g / pix}), flush=True)
+                      "lane_mean": tot_g / pix, "lane_percentiles": pct, "capped_split": split}), flush=True)
 
 
 if __name__ == "__main__":

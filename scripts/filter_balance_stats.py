@@ -44,12 +44,17 @@ def main():
     cx, cy = np.arange(V) % aw, np.arange(V) // aw
     nat, srt, tot_g, pix = 0.0, 0.0, 0.0, 0
     lanes = []
+    tiles = os.environ.get("TILES") == "1"
+    tile_nat, tile_2d = 0.0, 0.0
     for _ in range(nblk):
-        y = int(rng.integers(0, H))
+        y = int(rng.integers(0, H - 8)) if tiles else int(rng.integers(0, H))
         xb = int(rng.integers(0, W // 256)) * 256
         r = int(rng.integers(0, V))
         work, nds = [], []
-        for x in range(xb, xb + 256):
+        # TILES=1: a 64 x 8 block of pixels (row-major), compared as 8 row waves
+        # of 64 against 8 waves of 8 x 8 tiles
+        pixels = [(xb + i % 64, y + i // 64) for i in range(512)] if tiles else [(x, y) for x in range(xb, xb + 256)]
+        for x, y in pixels:
             p = y * W + x
             pv = projc[:, p]
             nz = pv[pv != 0]
@@ -80,6 +85,13 @@ def main():
                     break
             work.append(g)
         work = np.array(work, float)
+        if tiles:
+            blk = work.reshape(8, 64)
+            tile_nat += blk.max(1).sum()
+            tile_2d += blk.reshape(8, 8, 8).transpose(1, 0, 2).reshape(8, 64).max(1).sum()
+            tot_g += work.sum()
+            pix += 512
+            continue
         lanes.append(work)
         nds = np.array(nds)
         tot_g += work.sum()
@@ -90,6 +102,10 @@ def main():
         srt += sum(ws[64 * w:64 * w + 64].max() for w in range(4))
         order2 = np.argsort(-work, kind="stable")  # oracle: sorted by the true work
         ws2 = work[order2]
+    if tiles:
+        print(json.dumps({"blocks": nblk, "lane_mean": tot_g / pix, "wave_cost_rows_64x1": tile_nat / (8 * nblk),
+                          "wave_cost_tiles_8x8": tile_2d / (8 * nblk)}), flush=True)
+        return
     # a capped first pass (each wave stops after K gathers per lane; lanes not
     # done are queued) plus a second pass over the queue, packed 64 to a wave:
     # wave cost per 64 pixels, in gathers, with `prep` gathers' worth of

@@ -30,6 +30,7 @@ import json
 import os
 import socket
 import sys
+import threading
 import time
 
 import numpy as np
@@ -165,10 +166,49 @@ def run(args):
     try:
         res = bench(args, world, rank, local)
         if rank == 0:
-            print(json.dumps(res), flush=True)
+            _emit(res)
     finally:
         if world > 1:
             dist.destroy_process_group()
+        _WATCH["done"].set()
+
+
+_WATCH = {"done": threading.Event(), "printed": False, "lock": threading.Lock()}
+
+
+def _emit(res):
+    """Print the one JSON line (once: the sharded watchdog may print it first)."""
+    with _WATCH["lock"]:
+        if not _WATCH["printed"]:
+            _WATCH["printed"] = True
+            print(json.dumps(res), flush=True)
+
+
+def _guarded_view_sharded(args, e, world, rank, sync, res):
+    """The C4 sub-line, never at the cost of the headline line: an exception is
+    reported in the field, and at world > 1 -- where the sharded collectives
+    (async all-gathers, the point-to-point row exchange) run over RCCL -- a
+    watchdog armed until the process is done prints the line without the field
+    and ends the rank after MVS_SHARDED_TIMEOUT seconds (default 180) if they
+    hang, so every rank exits with the headline reported."""
+    if world > 1:
+        limit = float(os.environ.get("MVS_SHARDED_TIMEOUT", "180"))
+
+        def watch():
+            if _WATCH["done"].wait(limit):
+                return
+            if rank == 0:
+                out = dict(res)
+                out["view_sharded"] = {"error": f"no result within {limit:.0f} s; rank exited by the bench watchdog"}
+                _emit(out)
+            log(f"rank {rank}: sharded sub-line watchdog fired after {limit:.0f} s")
+            os._exit(0)
+
+        threading.Thread(target=watch, daemon=True).start()
+    try:
+        return view_sharded(args, e, world, rank, sync)
+    except Exception as ex:  # report, never hide; the headline stands
+        return {"error": repr(ex)}
 
 
 def dry_run(args, world, rank):
@@ -465,7 +505,7 @@ def bench(args, world, rank, local):
 
     # C4: one 32-view array sharded by reference view over the N GPUs (strong scaling)
     if not args.no_sharded and args.config in ("c2",) and cost == "ncc":
-        res["view_sharded"] = view_sharded(args, e, world, rank, sync)
+        res["view_sharded"] = _guarded_view_sharded(args, e, world, rank, sync, res)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -56,3 +56,36 @@ def test_world_size_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus", "2"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+_GUARD = """
+import sys, time
+sys.path.insert(0, {root!r})
+import bench
+def vs(*a):
+    if {mode!r} == "raise":
+        raise RuntimeError("collective failed")
+    time.sleep(60)
+bench.view_sharded = vs
+r = bench._guarded_view_sharded(None, None, 2, 0, None, {{"metric": "m", "value": 1.0}})
+print("returned", r, flush=True)
+bench._WATCH["done"].set()
+"""
+
+
+@pytest.mark.parametrize("mode", ["raise", "hang"])
+def test_sharded_subline_guard(mode):
+    """The C4 sub-line at world > 1 cannot take the headline line with it: an
+    exception comes back as {"error": ...}; a hang trips the watchdog, which
+    prints the line without the field and ends the rank with status 0."""
+    env = _env()
+    env["MVS_SHARDED_TIMEOUT"] = "2"
+    p = subprocess.run([sys.executable, "-c", _GUARD.format(root=ROOT, mode=mode)], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    if mode == "raise":
+        assert "returned {'error': \"RuntimeError('collective failed')\"}" in p.stdout
+    else:
+        (line,) = _json_lines(p.stdout)
+        assert line["value"] == 1.0 and "error" in line["view_sharded"]
+        assert "returned" not in p.stdout

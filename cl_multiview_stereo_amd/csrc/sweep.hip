@@ -391,17 +391,20 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
     if (!AFF) commit(0, 0);
   }
   __syncthreads();
-  for (int t = 0; t < T; t++) {
+  // chunks outer, neighbours inner (step t = c * nn + n): the chunk's reset
+  // and WTA fold sit outside the per-step body.  As one flat step loop the
+  // compiler if-converted them into every step (exec-masked compares and
+  // selects issued nn times per chunk)
+  int t = 0;
+  for (int c = 0; c < (a.nn > 0 ? a.nch : 0); c++) {
+#pragma unroll
+  for (int q = 0; q < PPW; q++)
+#pragma unroll
+    for (int o = 0; o < TH; o++) mn[q][o] = f32x2{SB_INIT, SB_INIT};
+  for (int n = 0; n < a.nn; n++, t++) {
     // step t+1's band lands in the other buffer (last read in step t-1, before
     // the previous barrier) while this step computes
     if (t + 1 < T) stage(t + 1, (t + 1) & 1);
-    const int c = t / a.nn, n = t - c * a.nn;
-    if (n == 0) {
-#pragma unroll
-      for (int q = 0; q < PPW; q++)
-#pragma unroll
-        for (int o = 0; o < TH; o++) mn[q][o] = f32x2{SB_INIT, SB_INIT};
-    }
     const SadRec& e = plan[t];
     const float4* bnd = band + (t & 1) * a.brows * a.bw;
     const int* tb = rtab + (t & 1) * DC * RR;
@@ -489,33 +492,35 @@ __global__ __launch_bounds__(256) void k_sad_band(const float4* __restrict__ lab
           p[o] = v;
         }
       }
+      // v_min_f32 as asm: fminf made the compiler canonicalise the
+      // loop-carried minima (a v_max_f32 x, x each) every step; no NaN here
 #pragma unroll
       for (int o = 0; o < TH; o++) {
-        mn[q][o].x = fminf(mn[q][o].x, p[o].x);
-        mn[q][o].y = fminf(mn[q][o].y, p[o].y);
-      }
-    }
-    if (n == a.nn - 1) {  // chunk complete: first-minimum WTA in level order
-#pragma unroll
-      for (int q = 0; q < PPW; q++) {
-        const int dl = c * DC + (wave * PPW + q) * 2;
-#pragma unroll
-        for (int o = 0; o < TH; o++) {
-          if (dl < a.D && mn[q][o].x < best[o]) {
-            best[o] = mn[q][o].x;
-            bidx[o] = dl;
-          }
-          if (dl + 1 < a.D && mn[q][o].y < best[o]) {
-            best[o] = mn[q][o].y;
-            bidx[o] = dl + 1;
-          }
-        }
+        asm("v_min_f32 %0, %1, %2" : "=v"(mn[q][o].x) : "v"(mn[q][o].x), "v"(p[o].x));
+        asm("v_min_f32 %0, %1, %2" : "=v"(mn[q][o].y) : "v"(mn[q][o].y), "v"(p[o].y));
       }
     }
     // step t+1's row table (its rows were last read in step t-1); the barrier
     // (vmcnt(0) first) publishes the table and the landed band
     if (t + 1 < T && !AFF) commit(t + 1, (t + 1) & 1);
     __syncthreads();
+  }
+  // chunk complete: first-minimum WTA in level order
+#pragma unroll
+  for (int q = 0; q < PPW; q++) {
+    const int dl = c * DC + (wave * PPW + q) * 2;
+#pragma unroll
+    for (int o = 0; o < TH; o++) {
+      if (dl < a.D && mn[q][o].x < best[o]) {
+        best[o] = mn[q][o].x;
+        bidx[o] = dl;
+      }
+      if (dl + 1 < a.D && mn[q][o].y < best[o]) {
+        best[o] = mn[q][o].y;
+        bidx[o] = dl + 1;
+      }
+    }
+  }
   }
   // merge the 4 waves' winners: lexicographic (cost, level)
   float* mb = (float*)smem;

@@ -440,8 +440,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
   };
 
-  reset();
   if (T == 0) {  // no neighbours: every window invalid, cost 2
+    reset();
 #pragma unroll
     for (int o = 0; o < TH; o++) sr[o] = __int_as_float(0x7fc00000);
     if (FUSE) {  // the fused store reads s_r from LDS
@@ -500,16 +500,29 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   }
   __syncthreads();
 
-  int n = 0, c = 0;
-  for (int t = 0; t < T; t++) {
+  // one pipeline step t = c * nn + n: prefetch step t+1's bands, then this
+  // step's correlations into E.  FIRST (the chunk's first neighbour) assigns
+  // E instead of max-ing into it, so no -inf reset of the 8 DPW accumulators
+  // per chunk and no max for the first neighbour: v_max_f32 drops a NaN
+  // (invalid neighbour window), so max(-inf, x) and x differ only when x is
+  // NaN, and a NaN that survives to the store gives the same cost 2 as -inf
+  // (both clamp to -1 there), while a later finite x replaces it either way.
+  // Only the K = 5 EVEN kernels (horizontal neighbours: the C2 headline) are
+  // peeled.  The others keep the flat loop: their second copy of the step
+  // spilled at the 128-VGPR cap (fused K = 7 scratch 104 -> 532 bytes, K = 5
+  // non-EVEN DPW 4 72 -> 452)
+  constexpr bool PEEL = K == 5 && EVEN;
+  auto step = [&](int t, int n, int cprev, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
     const int n1 = n + 1 == nn ? 0 : n + 1;
     if (t + 1 < T) stage(t + 1, n1, (t + 1) & 1);  // prefetch step t+1 while computing t
-    // the previous chunk's costs are written here, after this step's prefetch
-    // is issued and a whole step before the barrier's vmcnt(0) (which also
-    // waits for stores): the write latency hides behind the compute
-    if (n == 0 && t > 0) {
-      store(c - 1);
-      reset();
+    // the previous chunk's costs are written here (its E, before this step
+    // overwrites it), after this step's prefetch is issued and a whole step
+    // before the barrier's vmcnt(0) (which also waits for stores): the write
+    // latency hides behind the compute.  (FUSE: the register fold.)
+    if ((FIRST || !PEEL) && cprev >= 0) {
+      store(cprev);
+      if (!PEEL) reset();
     }
     const u32x4* npk = nbase + (t & 1) * nbuf;
     const u32x4* nst = npk + a.pk_pairs * BW;
@@ -548,15 +561,34 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
         const float f1 = __int_as_float(ps[o + 1 + 2 * R]) - __int_as_float(ps[o]);
         const f32x2 f = f32x2{f0, f1};
         const f32x2 xv = __builtin_elementwise_fma(rsn[m], f32x2{sv[m].z, sv[m].w}, f * f32x2{sv[m].x, sv[m].y});
-        E[j][o] = vmax(E[j][o], xv.x);
-        E[j][o + 1] = vmax(E[j][o + 1], xv.y);
+        if (FIRST) {
+          E[j][o] = xv.x;
+          E[j][o + 1] = xv.y;
+        } else {
+          E[j][o] = vmax(E[j][o], xv.x);
+          E[j][o + 1] = vmax(E[j][o + 1], xv.y);
+        }
       }
     }
-    if (n1 == 0) c++;  // chunk c complete
-    n = n1;
     __syncthreads();  // step t+1's bands landed (vmcnt 0); this buffer free for t+2
+  };
+  if (PEEL) {  // chunks outer, neighbours inner, the first neighbour peeled
+    int t = 0;
+    for (int c = 0; c < a.nch; c++) {
+      step(t++, 0, c - 1, std::true_type{});
+      for (int n = 1; n < nn; n++) step(t++, n, -1, std::false_type{});
+    }
+  } else {  // one flat step loop, E reset after each chunk's store
+    reset();
+    for (int t = 0, n = 0, c = 0; t < T; t++) {
+      step(t, n, n == 0 && t > 0 ? c - 1 : -1, std::false_type{});
+      if (++n == nn) {
+        n = 0;
+        c++;
+      }
+    }
   }
-  store(c - 1);
+  store(a.nch - 1);
   }
   if (FUSE) {
     // merge the NW waves' partials of each of the tile's 64 x TH pixels; the

@@ -11,7 +11,9 @@ hypotheses x 4 neighbours and its winner-take-all + confidence.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--cost ncc|sad]
 
 `value` is the fused step (mvs_ncc_wta_d: the sweep kernel folds the WTA in,
-no cost volume in HBM).  The same invocation also times the two-pass step
+no cost volume in HBM), with the superpixel chain on a side HIP stream beside
+the per-pixel chain (--serial: one stream; `serial_variant` times that form
+too, and `roofline_sweep` comes from it).  The same invocation also times the two-pass step
 (materialised [D][H][W] volume + the k_wta streaming pass, bit-identical maps):
 `roofline` is k_wta's HBM read of that volume, the north star's roofline.
 
@@ -84,7 +86,11 @@ def parse(argv=None):
     ap.add_argument("--two-pass", action="store_true",
                     help="headline = the two-pass step (cost volume in HBM + k_wta) instead of the fused sweep")
     ap.add_argument("--concurrent", action="store_true",
-                    help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py)")
+                    help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py); "
+                         "the default for the fused NCC headline of the unsharded configs")
+    ap.add_argument("--serial", action="store_true",
+                    help="one stream for the whole step (the fused headline otherwise runs the superpixel "
+                         "chain on a side stream)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher, rank setup, gathers and max-over-ranks timing on gloo")
     return ap.parse_args(argv)
@@ -372,10 +378,16 @@ def bench(args, world, rank, local):
     def avg(lst):
         return sum(s.elapsed_time(t) for s, t, _ in lst) / len(lst) * 1e-3
 
-    def make(fz):
+    # the fused NCC headline runs the superpixel chain (SLIC, extents,
+    # superpixel sweep) on a side stream beside the per-pixel chain
+    # (pipeline.py, concurrent=True): C2 2.55 -> 2.52 ms per step in three
+    # interleaved rounds (profiles/r03j_concurrent.txt); --serial turns it off
+    conc_head = args.concurrent or (fused and not sharded and cost == "ncc" and not args.serial)
+
+    def make(fz, conc=False):
         p = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,
                      refine=bool(cfg.get("refine")), filt=bool(cfg.get("filt")) and not sharded,
-                     concurrent=args.concurrent, fused=fz)
+                     concurrent=conc, fused=fz)
         if not sharded:
             return p, (lambda: p.exe_pipeline(rgbx))
         from cl_multiview_stereo_amd.distributed import EngineBackend, ShardedPipeline, ViewGather
@@ -383,7 +395,7 @@ def bench(args, world, rank, local):
                              filt=bool(cfg.get("filt")))
         return p, (lambda: sp.run(rgbx))
 
-    pipe, step = make(fused)
+    pipe, step = make(fused, conc_head)
     recording[0] = True
     elapsed, out = timed(step, args.steps, args.warmup, dev, world, sync)
     recording[0] = False
@@ -391,6 +403,24 @@ def bench(args, world, rank, local):
     units = V if sharded else world * V  # reference views processed per step, whole job
     mpix = units * W * H * args.steps / elapsed / 1e6
     head_timers = {k: list(v) for k, v in timers.items()}
+    serial = None
+    if conc_head:
+        # the same step on one stream: the fused kernel's own time for
+        # roofline_sweep (beside the side stream it shares the CUs)
+        _, ser_step = make(fused, False)
+        for k in timers:
+            timers[k].clear()
+        recording[0] = True
+        ser_el, ser_out = timed(ser_step, args.steps, max(1, args.warmup), dev, world, sync)
+        recording[0] = False
+        head_timers = {k: list(v) for k, v in timers.items()}
+        serial = {"what": "the same step on one HIP stream (the headline runs the superpixel chain on a side "
+                          "stream beside the per-pixel chain)",
+                  "value": round(units * W * H * args.steps / ser_el / 1e6, 3), "unit": "Mpix/s",
+                  "ms_per_step": round(ser_el * 1e3 / max(args.steps, 1), 4),
+                  "bit_identical_to_headline": bool(all(
+                      torch.equal(getattr(ser_out, f).view(torch.int32), getattr(out, f).view(torch.int32))
+                      for f in ("disp", "conf") if getattr(out, f, None) is not None))}
 
     res = {
         "metric": METRIC,
@@ -415,8 +445,11 @@ def bench(args, world, rank, local):
                              "two-pass (cost volume in HBM + k_wta)") if cost == "ncc" else cost,
                    "parallelism": (f"views sharded over {world} GPU(s)" if sharded else
                                    f"view-stack per GPU x{world}"),
-                   "refinement": bool(cfg.get("refine")), "consistency_filter": bool(cfg.get("filt"))},
+                   "refinement": bool(cfg.get("refine")), "consistency_filter": bool(cfg.get("filt")),
+                   "streams": "superpixel chain on a side stream" if conc_head else "one"},
     }
+    if serial is not None:
+        res["serial_variant"] = serial
     if fused and head_timers["fused"]:
         t_f = avg(head_timers["fused"])  # per call (one run of reference views)
         vpc = sum(n for _, _, n in head_timers["fused"]) / len(head_timers["fused"])
@@ -428,7 +461,8 @@ def bench(args, world, rank, local):
             "bound": "valu", "avg_call_ms": round(t_f * 1e3, 4), "views_per_call": vpc,
             "avg_ms_per_view": round(t_f * 1e3 / vpc, 4),
             "view_cells_per_s": round(cells * nbr * vpc / t_f / 1e9, 3), "unit_view_cells": "G view-cells/s",
-            "timing": "HIP events around each mvs_ncc_wta_range_d call of the timed steps, on its stream"}
+            "timing": "HIP events around each mvs_ncc_wta_range_d call of the timed steps, on its stream" +
+                      (" (the serial_variant pass: one stream, the kernel alone on the GPU)" if conc_head else "")}
         if per_view is not None:
             res["roofline_sweep"].update({
                 "valu_wave_insts_per_view": round(per_view["insts"]),
@@ -441,7 +475,7 @@ def bench(args, world, rank, local):
     if cost == "ncc":
         tp_out = out
         if fused:
-            _, tp_step = make(False)
+            _, tp_step = make(False, False)
             for k in timers:
                 timers[k].clear()
             recording[0] = True

@@ -87,7 +87,7 @@ def parse(argv=None):
                     help="headline = the two-pass step (cost volume in HBM + k_wta) instead of the fused sweep")
     ap.add_argument("--concurrent", action="store_true",
                     help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py); "
-                         "the default for the fused NCC headline of the unsharded configs without refinement")
+                         "the default for the fused NCC headline of the unsharded configs")
     ap.add_argument("--serial", action="store_true",
                     help="one stream for the whole step (the fused headline otherwise runs the superpixel "
                          "chain on a side stream)")
@@ -382,11 +382,9 @@ def bench(args, world, rank, local):
     # superpixel sweep) on a side stream beside the per-pixel chain
     # (pipeline.py, concurrent=True): C2 2.55 -> 2.52 ms per step in three
     # interleaved rounds (profiles/r03j_concurrent.txt); --serial turns it off
-    # Configurations with refinement (c3) keep one stream unless --concurrent:
-    # there the step continues past the join, and c3 measured 3.64 concurrent
-    # against 3.49 ms serial in one run (profiles/r03m_configs.txt)
-    conc_head = args.concurrent or (fused and not sharded and cost == "ncc" and not cfg.get("refine")
-                                    and not args.serial)
+    # (c3, with refinement and the filter after the join: 3.462-3.469 ->
+    # 3.431-3.434 ms in three interleaved rounds, profiles/r03n_ref_c3.txt)
+    conc_head = args.concurrent or (fused and not sharded and cost == "ncc" and not args.serial)
 
     def make(fz, conc=False):
         p = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,

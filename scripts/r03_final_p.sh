@@ -1,0 +1,12 @@
+#!/usr/bin/env bash
+# Last pass of the session on the committed tree: GPU suite, smoke, the driver's command.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/r03p; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+echo smoke ok
+timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+python3 -c "import json;j=json.load(open('$O/bench.json'));print(j['value'], j['ms_per_step'], j['depth_l1_vs_oracle']['bit_exact'], j['roofline']['frac'], j['roofline_sweep']['avg_ms_per_view'])"

@@ -83,6 +83,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sharded", action="store_true", help="skip the C4 view-sharded strong-scaling line")
     ap.add_argument("--no-reference-cost", action="store_true", help="skip the C2 --cost sad sub-line")
+    ap.add_argument("--no-reference-defaults", action="store_true",
+                    help="skip the `reference_defaults` sub-line (--config ref inside the c2 line)")
     ap.add_argument("--two-pass", action="store_true",
                     help="headline = the two-pass step (cost volume in HBM + k_wta) instead of the fused sweep")
     ap.add_argument("--concurrent", action="store_true",
@@ -539,6 +541,15 @@ def bench(args, world, rank, local):
         res["reference_cost"] = reference_cost(args, e, st, stack, rgbx, cfg, world, sync,
                                                check=rank == 0 and not args.no_cpu_baseline)
 
+    # the reference's own algorithm at its own defaults (clMVDE.cpp:14-36), so a
+    # regression of its kernels (k_propagate above all) shows in the driver's line
+    if args.config == "c2" and cost == "ncc" and world == 1 and not args.no_reference_defaults:
+        try:
+            res["reference_defaults"] = reference_defaults(args, e, world, sync,
+                                                           check=rank == 0 and not args.no_cpu_baseline)
+        except Exception as ex:  # report, never hide; the headline stands
+            res["reference_defaults"] = {"error": repr(ex)}
+
     # C4: one 32-view array sharded by reference view over the N GPUs (strong scaling)
     if not args.no_sharded and args.config in ("c2",) and cost == "ncc":
         res["view_sharded"] = _guarded_view_sharded(args, e, world, rank, sync, res)
@@ -591,6 +602,35 @@ def reference_cost(args, e, st, stack, rgbx, cfg, world, sync, check=True):
                                    "bit_exact": bool(np.array_equal(got, want[:, :keep])),
                                    "sample": f"rows 0..{keep - 1} of all {V} reference views, {W} wide "
                                              f"(oracle: {time.perf_counter() - t0:.1f} s on the host)"}
+    return r
+
+
+def reference_defaults(args, e, world, sync, check=True):
+    """`--config ref` inside the default line: clMVDE main()'s defaults (3x3
+    array 1080p, S = 8, levels 30..60, bl 1.0359, superpixel SAD sweep +
+    refinement with 5 propagations + fusion of all 9 views).  5 timed steps
+    after 1 warmup; with `check`, the fused maps of the last step against the
+    oracle's full-size run (~5 s on the host)."""
+    import torch
+
+    from cl_multiview_stereo_amd import params, synth
+    from cl_multiview_stereo_amd.pipeline import Pipeline
+    c = CONFIGS["ref"]
+    V, W, H = c["aw"] * c["ah"], c["W"], c["H"]
+    st = params.Settings(spixl_size=c["S"], array_width=c["aw"], array_height=c["ah"], min_disp=c["dmin"],
+                         max_disp=c["dmax"], inc=1, neib_hor=c["nh"], neib_ver=c["nv"], bl_ratio=c["bl"],
+                         window=c["K"], cost="none")
+    stack, _ = synth.make_stack(W, H, c["aw"], c["ah"], c["dmin"], c["dmax"], c["bl"], 0x5EED + 2)  # = --config ref
+    rgbx = torch.from_numpy(stack).to(e.device)
+    p = Pipeline(e, st, W, H, pixel_cost=None, refine=True, filt=False, fused=False)
+    steps = 5
+    el, out = timed(lambda: p.exe_pipeline(rgbx), steps, 1, e.device, world, sync)
+    r = {"what": c["workload"], "value": round(V * W * H * steps / el / 1e6, 3), "unit": "Mpix/s",
+         "ms_per_step": round(el * 1e3 / steps, 4), "steps": steps, "dtype": "f32 (f64 where the reference promotes)"}
+    if check:
+        cpu, l1 = cpu_baseline(p, stack, c, "none", out)
+        r["depth_l1_vs_oracle"] = l1
+        r["cpu_baseline"] = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")}
     return r
 
 

@@ -91,7 +91,7 @@ __global__ void k_flatness(const float* __restrict__ spixl, int mw, int mh, floa
 }
 
 // ---- init_smoothness + initialize_consistency + init_current_state ---------
-__device__ float init_smoothness(const RArgs& c, const float* __restrict__ spixl, const float* sp, float2 fl, int x,
+__device__ __forceinline__ float init_smoothness(const RArgs& c, const float* __restrict__ spixl, const float* sp, float2 fl, int x,
                                  int y, int z, int nks, float kss) {
   long M = (long)c.mw * c.mh;
   float sm = 0.0f, wn = 0.0f;
@@ -148,7 +148,7 @@ __device__ __forceinline__ uint32_t label_at(const void* labels, long i) {
 }
 
 template <typename LT>
-__device__ float init_consistency(const RArgs& c, const float* __restrict__ spixl, const void* __restrict__ labels,
+__device__ __forceinline__ float init_consistency(const RArgs& c, const float* __restrict__ spixl, const void* __restrict__ labels,
                                   const uint8_t* rp, const int* __restrict__ vs, const int* __restrict__ sn, int z,
                                   const float* color, float cxf, float cyf, float d, float2 fl) {
   long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
@@ -242,7 +242,7 @@ struct PCtx {
   float2 fl;
 };
 
-__device__ float comp_smoothness(const PCtx& p, float d, float nx, float ny, float nz) {
+__device__ __forceinline__ float comp_smoothness(const PCtx& p, float d, float nx, float ny, float nz) {
   const RArgs& c = p.c;
   long M = (long)c.mw * c.mh;
   float sm = 0.0f, wn = 0.0f;
@@ -290,7 +290,7 @@ __device__ float comp_smoothness(const PCtx& p, float d, float nx, float ny, flo
 // round trips.  A label is the superpixel index y*mw + x, so the record is at
 // view * M + label (the reference's % and / recombine to it exactly).
 template <typename LT>
-__device__ float comp_consistency(const PCtx& p, float d, float nx, float ny, float nz) {
+__device__ __forceinline__ float comp_consistency(const PCtx& p, float d, float nx, float ny, float nz) {
   const RArgs& c = p.c;
   const long M = (long)c.mw * c.mh, P = (long)c.W * c.H;
   float cons = 0.0f;

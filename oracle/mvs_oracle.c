@@ -585,7 +585,61 @@ typedef struct {
   float bl, fuse, alpha, gamma;
 } rctx;
 
-static float expf_neg_sq(float diff, float k) { return mvs_expf(((-diff) * diff) * k); }
+/* Numerics probes of the refinement (oracle/Makefile `probes`, tests/ref_artifacts.py
+ * --probes; never defined in the pinned build): each swaps one implementation-
+ * defined choice of the pinned definition for the alternative a reference
+ * device may have made, to measure how far that alone moves the refinement.
+ *   MVS_PROBE_RCP_DIV       every fp32 quotient of the refinement as a * RN(1/b)
+ *                           (the form the SLIC centre means are pinned to)
+ *   MVS_PROBE_LIBM_EXP      exp / expf from the C library (glibc) instead of mvs_detmath
+ *   MVS_PROBE_EXP_ULP=k     every expf result moved by a hash-chosen -k..+k ulp
+ *   MVS_PROBE_SQRT_RSQ      sqrt(s) as s * RN(1/sqrt(s)) (an rsqrt-based sqrt)
+ *   MVS_PROBE_REFINE_CONTRACT  (clang -mfma) mul+add contracted from here on */
+#ifdef MVS_PROBE_REFINE_CONTRACT
+#pragma clang fp contract(on)
+#endif
+#ifdef MVS_PROBE_RCP_DIV
+#define RDIV(a, b) ((a) * (1.0f / (b)))
+#else
+#define RDIV(a, b) ((a) / (b))
+#endif
+#ifdef MVS_PROBE_SQRT_RSQ
+static float rsqrtf_(float s) { return s > 0.0f ? s * (1.0f / sqrtf(s)) : sqrtf(s); }
+#define RSQRT(s) rsqrtf_(s)
+#else
+#define RSQRT(s) sqrtf(s)
+#endif
+#ifdef MVS_PROBE_LIBM_EXP
+#define REXP_BASE(x) expf(x)
+#define REXP_D(x) exp(x)
+#else
+#define REXP_BASE(x) mvs_expf(x)
+#define REXP_D(x) mvs_exp(x)
+#endif
+static float rexpf(float x) {
+  float r = REXP_BASE(x);
+#ifdef MVS_PROBE_EXP_ULP
+  uint32_t u, v;
+  memcpy(&u, &x, 4);
+  u = (u ^ (u >> 15)) * 2654435761u;
+  int k = (int)((u >> 8) % (2 * MVS_PROBE_EXP_ULP + 1)) - MVS_PROBE_EXP_ULP;
+  if (r > 0.0f && r < 3.0e38f) {
+    memcpy(&v, &r, 4);
+    v = (uint32_t)((int32_t)v + k);
+    memcpy(&r, &v, 4);
+  }
+#endif
+  return r;
+}
+static float rdist3(float ax, float ay, float az, float bx, float by, float bz) {
+  float dx = ax - bx, dy = ay - by, dz = az - bz;
+  float s = dx * dx;
+  s = s + dy * dy;
+  s = s + dz * dz;
+  return RSQRT(s);
+}
+
+static float expf_neg_sq(float diff, float k) { return rexpf(((-diff) * diff) * k); }
 
 /* compute_flatness, clcode.cl:1076-1132 */
 void orc_flatness(int V, int mw, int mh, const float* spixl, float gamma, float* flat) {
@@ -607,8 +661,8 @@ void orc_flatness(int V, int mw, int mh, const float* spixl, float gamma, float*
           diff = diff + (c1[2] - c0[2]) * (c1[2] - c0[2]);
           fl = fl + diff;
         }
-        flat[2 * idx] = mvs_expf((-fl) * gamma);
-        flat[2 * idx + 1] = (float)(1.0 - mvs_exp((-0.25 * (double)fl) * (double)gamma));
+        flat[2 * idx] = rexpf((-fl) * gamma);
+        flat[2 * idx + 1] = (float)(1.0 - REXP_D((-0.25 * (double)fl) * (double)gamma));
       }
 }
 
@@ -627,7 +681,7 @@ static float init_smoothness(const rctx* c, const float* sp_ref, const float* fl
       int px = x + i, py = y + j;
       if (px >= 0 && py >= 0 && px < c->mw && py < c->mh && (i != 0 || j != 0)) {
         const float* s = c->spixl + 8 * (c->M * z + (long)c->mw * py + px);
-        float diff = mvs_distance3(s[3], s[4], s[5], cl0, cl1, cl2);
+        float diff = rdist3(s[3], s[4], s[5], cl0, cl1, cl2);
         float simi = expf_neg_sq(diff, c->gamma);
         diff = disp - s[7];
         sm = sm + simi * expf_neg_sq(diff, c->alpha);
@@ -643,14 +697,14 @@ static float init_smoothness(const rctx* c, const float* sp_ref, const float* fl
     for (int k = 0; k < 4; k++) {
       if (!ok[k]) continue;
       const float* s = c->spixl + 8 * (c->M * z + (long)c->mw * cand[k][1] + cand[k][0]);
-      float diff = mvs_distance3(cl0, cl1, cl2, s[3], s[4], s[5]);
+      float diff = rdist3(cl0, cl1, cl2, s[3], s[4], s[5]);
       float simi = expf_neg_sq(diff, gi);
       diff = disp - s[7];
       sm = sm + simi * expf_neg_sq(diff, c->alpha);
       wn = wn + simi;
     }
   }
-  return wn > 0 ? sm / wn : 0.000001f;
+  return wn > 0 ? RDIV(sm, wn) : 0.000001f;
 }
 
 static void samples_of(const uint8_t* r, int* s) {
@@ -660,7 +714,7 @@ static void samples_of(const uint8_t* r, int* s) {
 
 static float finish_consistency(float cons, int vc) {
   float margin = 0.01f;
-  if (vc > 0) return fmaxf(margin, cons / (float)vc);
+  if (vc > 0) return fmaxf(margin, RDIV(cons, (float)vc));
   return margin;
 }
 
@@ -692,14 +746,14 @@ static float init_consistency(const rctx* c, int x, int y, int z, const float* c
           visible = visible + wv * expf_neg_sq(diff, c->alpha);
           vis_w = vis_w + wv;
           occ_w = occ_w + (1.0f - wv);
-          diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+          diff = rdist3(s[3], s[4], s[5], color[0], color[1], color[2]);
           visibility = visibility + expf_neg_sq(diff, c->gamma);
           num = num + 1.0f;
         }
       }
     if (num > 0) {
       vc++;
-      if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+      if (vis_w > 0) cons = cons + (RDIV(vis_w, num) * RDIV(visibility, vis_w)) * RDIV(visible, vis_w);
       if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)fl[1]);
     }
   }
@@ -731,7 +785,7 @@ static float plane_at(const float* n, float cx, float cy, float d, float px, flo
   float t = n[0] * (cx - px);
   t = t + n[1] * (cy - py);
   t = t + n[2] * d;
-  return t / n[2];
+  return RDIV(t, n[2]);
 }
 
 /* compute_smoothness, clcode.cl:1407-1525 */
@@ -744,7 +798,7 @@ static float comp_smoothness(const rctx* c, const float* st, float d, const floa
       if (px >= 0 && py >= 0 && px < c->mw && py < c->mh && (i != 0 || j != 0)) {
         long q = c->M * z + (long)c->mw * py + px;
         const float* s = c->spixl + 8 * q;
-        float diff = mvs_distance3(color[0], color[1], color[2], s[3], s[4], s[5]);
+        float diff = rdist3(color[0], color[1], color[2], s[3], s[4], s[5]);
         float simi = expf_neg_sq(diff, c->gamma);
         float di = plane_at(nv, center[0], center[1], d, s[1], s[2]);
         diff = di - st[6 * q];
@@ -762,7 +816,7 @@ static float comp_smoothness(const rctx* c, const float* st, float d, const floa
       if (!ok[k]) continue;
       long q = c->M * z + (long)c->mw * cand[k][1] + cand[k][0];
       const float* s = c->spixl + 8 * q;
-      float diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+      float diff = rdist3(s[3], s[4], s[5], color[0], color[1], color[2]);
       float simi = expf_neg_sq(diff, gi);
       float de = plane_at(nv, center[0], center[1], d, s[1], s[2]);
       diff = de - st[6 * q];
@@ -770,7 +824,7 @@ static float comp_smoothness(const rctx* c, const float* st, float d, const floa
       wn = wn + simi;
     }
   }
-  return wn > 0 ? sm / wn : 0.000001f;
+  return wn > 0 ? RDIV(sm, wn) : 0.000001f;
 }
 
 /* compute_consistency, clcode.cl:1528-1631 (view_subset stride = V) */
@@ -806,14 +860,14 @@ static float comp_consistency(const rctx* c, const float* st, const uint8_t* rep
           visible = visible + wv * expf_neg_sq(diff, c->alpha);
           vis_w = vis_w + wv;
           occ_w = occ_w + (1.0f - wv);
-          diff = mvs_distance3(s[3], s[4], s[5], color[0], color[1], color[2]);
+          diff = rdist3(s[3], s[4], s[5], color[0], color[1], color[2]);
           visibility = visibility + expf_neg_sq(diff, c->gamma);
           num = num + 1.0f;
         }
       }
     if (num > 0) {
       vc++;
-      if (vis_w > 0) cons = cons + ((vis_w / num) * (visibility / vis_w)) * (visible / vis_w);
+      if (vis_w > 0) cons = cons + (RDIV(vis_w, num) * RDIV(visibility, vis_w)) * RDIV(visible, vis_w);
       if (occ_w > 0) cons = (float)((double)cons + 0.5 * (double)fl[1]);
     }
   }
@@ -833,10 +887,10 @@ static void plane_update(const rctx* c, const float* st, const uint8_t* rep, int
   float t = n1[0] * (sc[1] - center[0]);
   t = t + n1[1] * (sc[2] - center[1]);
   t = t + n1[2] * d1;
-  float di = t / n1[2];
+  float di = RDIV(t, n1[2]);
   float sm1 = comp_smoothness(c, st, di, n1, center, color, x, y, z, fl, nks, kss);
   float cs1 = comp_consistency(c, st, rep, di, n1, center, color, x, y, z, fl);
-  float diff = mvs_distance3(color[0], color[1], color[2], sc[3], sc[4], sc[5]);
+  float diff = rdist3(color[0], color[1], color[2], sc[3], sc[4], sc[5]);
   float simi = expf_neg_sq(diff, c->gamma);
   if ((iter < 4 && sm1 * simi > cur->sm) || cs1 * sm1 > cur->sm * cur->cs) {
     cur->d = di; cur->sm = sm1; cur->cs = cs1;
@@ -850,8 +904,8 @@ static void normalize4(float* v) {
   s = s + v[2] * v[2];
   s = s + v[3] * v[3];
   if (s == 0.0f) return;
-  float r = sqrtf(s);
-  v[0] = v[0] / r; v[1] = v[1] / r; v[2] = v[2] / r; v[3] = v[3] / r;
+  float r = RSQRT(s);
+  v[0] = RDIV(v[0], r); v[1] = RDIV(v[1], r); v[2] = RDIV(v[2], r); v[3] = RDIV(v[3], r);
 }
 
 /* spatialRefinement + cross_product_test, clcode.cl:1676-1723 */
@@ -940,9 +994,13 @@ void orc_spixl_to_image(int V, int W, int H, int S, const float* spixl, const ui
         float v = t[3] * (s[1] - (float)x);
         v = v + t[4] * (s[2] - (float)y);
         v = v + t[5] * t[0];
-        disp[P * z + (long)W * y + x] = v / t[5];
+        disp[P * z + (long)W * y + x] = RDIV(v, t[5]);
       }
 }
+
+#ifdef MVS_PROBE_REFINE_CONTRACT
+#pragma clang fp contract(off)
+#endif
 
 /* project_to_reference_inv + remove_view_inconsistency, clcode.cl:1995-2101,
  * pinned order: every projection slice first, then every stability vote. */

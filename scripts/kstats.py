@@ -2,12 +2,16 @@
 """Per-kernel dispatch count / average / total from a rocprofv3 --kernel-trace
 database (run_results.db): python3 scripts/kstats.py DB [name-substring ...]."""
 import collections
+import glob
+import os
 import sqlite3
 import sys
 
 
 def main():
     db = sys.argv[1]
+    if os.path.isdir(db):  # a rocprofv3 -d directory: its (one) database
+        db = sorted(glob.glob(os.path.join(db, "**", "*.db"), recursive=True))[-1]
     keys = sys.argv[2:]
     c = sqlite3.connect(db)
     acc = collections.OrderedDict()

@@ -188,6 +188,12 @@ __device__ __forceinline__ float vmax(float acc, float e) {
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(e));
   return r;
 }
+// max(-1, e) with -1.0 as an inline constant (no VGPR holding it)
+__device__ __forceinline__ float vmax_m1(float e) {
+  float r;
+  asm("v_max_f32 %0, -1.0, %1" : "=v"(r) : "v"(e));
+  return r;
+}
 __device__ __forceinline__ float vmin(float acc, float e) {
   float r;
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(e));
@@ -212,13 +218,21 @@ constexpr float kWtaInit = 1000000.0f;  // k_wta's Top4 initial cost (sweep.hip)
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// Row-parity modes of a launch's bands (k_ncc_volume's PAR; the plan knows it):
+//   kParEven  every level's pk and stats rows start on a pair boundary (K = 5
+//             with horizontal neighbours: R + tymax even)
+//   kParOdd   every pk start is odd and every stats start even (K = 7 with
+//             horizontal neighbours: R = 3)
+//   kParMixed either, per level (vertical / diagonal neighbours): a run-time test
+constexpr int kParMixed = 0, kParEven = 1, kParOdd = 2;
+
 // N consecutive band rows starting at band row r0 of a row-pair band (pair
 // row stride BW, one column): ds_read_b128 per pair; an odd start takes the
 // first and last rows as ds_read_b64 halves.  N even.
-template <int N, int BW, bool EVEN>
+template <int N, int BW, int PAR>
 __device__ __forceinline__ void read_rows(const u32x4* col, int r0, u32x2 (&v)[N]) {
   const u32x4* p = col + (r0 >> 1) * BW;
-  if (EVEN || (r0 & 1) == 0) {
+  if (PAR == kParEven || (PAR == kParMixed && (r0 & 1) == 0)) {
 #pragma unroll
     for (int i = 0; i < N / 2; i++) {
       const u32x4 t = p[i * BW];
@@ -243,10 +257,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // The N/2 stats row pairs (o, o+1), o even, of a band column starting at band
 // row r0: {a(o), a(o+1), b(o), b(o+1)}.  An odd start joins the second row of
 // one stored pair with the first row of the next.
-template <int N, int BW, bool EVEN>
+template <int N, int BW, int PAR>
 __device__ __forceinline__ void read_stat_pairs(const u32x4* col, int r0, f32x4 (&v)[N / 2]) {
   const u32x4* p = col + (r0 >> 1) * BW;
-  if (EVEN || (r0 & 1) == 0) {
+  if (PAR != kParMixed || (r0 & 1) == 0) {
 #pragma unroll
     for (int i = 0; i < N / 2; i++) v[i] = __builtin_bit_cast(f32x4, p[i * BW]);
   } else {
@@ -278,8 +292,7 @@ __device__ __forceinline__ int dot4(unsigned a, unsigned b, int c) {
   return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
 }
 
-// EVEN: every level's band rows start on a pair boundary (all horizontal
-// neighbours with even R + tymax): branch-free pair reads.
+// PAR: the bands' row parity (kParEven / kParOdd: branch-free pair reads).
 // FUSE: instead of writing the volume, every wave folds its levels' costs into
 // a per-pixel (smallest cost, its level, second smallest cost) in level order;
 // the workgroup then merges its waves through LDS into disp/conf.  A wave's
@@ -287,7 +300,7 @@ __device__ __forceinline__ int dot4(unsigned a, unsigned b, int c) {
 // smallest cost outside best+-1 is, per wave, its second smallest if its best
 // level is in that window, else its smallest -- exactly what k_wta's top-4
 // yields (ties resolved to the lower level by the strict < in level order).
-template <int K, int TH, int DPW, int NW, int BW, bool EVEN, bool FUSE>
+template <int K, int TH, int DPW, int NW, int BW, int PAR, bool FUSE>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_volume(const uint2* __restrict__ stats, const uint2* __restrict__ pk,
                                                     const NccRec* __restrict__ plan, NccArgs a,
                                                     float* __restrict__ vol, WtaOut wo) {
@@ -367,6 +380,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   float* srl = (float*)(smem + 16 * (size_t)max(2 * nbuf, FUSE ? 3 * NW * TH * 64 / 4 : 0));
   float wv0[TH], wv1[TH];  // FUSE: this wave's smallest and second smallest cost per row
   int wi0[TH];             //       level of the smallest
+  // fused K = 7: the levels of rows 2m, 2m+1 as the halves of one register
+  // (0xffff: none yet).  With one register per row the fold went past the
+  // 128-VGPR cap (r03: 96 B of scratch, three of them spilled and reloaded at
+  // every chunk's fold -- C5's fused launch moved 40 GB of scratch writes
+  // against 0.5 GB of output); a half-select costs one v_bfi_b32 more per cell
+  constexpr bool PKI = FUSE && K == 7;
+  unsigned wi0p[TH / 2];
   if (FUSE) {
 #pragma unroll
     for (int o = 0; o < TH; o++) {
@@ -374,6 +394,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
       wv1[o] = kWtaInit;
       wi0[o] = -1;
     }
+#pragma unroll
+    for (int m = 0; m < TH / 2; m++) wi0p[m] = 0xffffffffu;
   }
   auto reset = [&]() {
 #pragma unroll
@@ -385,37 +407,47 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // -inf * 0 and of an invalid reference window); partial tiles/chunks masked
   auto store = [&](int c) {
     if (x >= W) return;
-    float srv[TH];  // FUSE: s_r of the tile's rows, read once per chunk
     if (FUSE) {
+      // the fold, one quad of rows at a time: s_r of 4 rows (one ds_read_b128)
+      // folded for every level before the next quad's are loaded, so at most 4
+      // s_r registers are live beside E and the triple (at K = 7 the whole
+      // tile's 8 pushed the fold past the 128-VGPR cap: r03, 96 B of scratch,
+      // three accumulators spilled and reloaded at every chunk's fold -- C5's
+      // fused launch moved 40 GB of scratch writes against 0.5 GB of output)
       const int ln = lane_now();
 #pragma unroll
-      for (int o = 0; o < TH; o += 4) {
-        const f32x4 t = *(const f32x4*)(srl + ln * TH + o);
-        srv[o] = t.x;
-        srv[o + 1] = t.y;
-        srv[o + 2] = t.z;
-        srv[o + 3] = t.w;
+      for (int q = 0; q < TH; q += 4) {
+        const f32x4 sq = *(const f32x4*)(srl + ln * TH + q);
+#pragma unroll
+        for (int j = 0; j < DPW; j++) {
+          const int dl = c * DC + wave + NW * j;
+          if (dl >= a.D) break;
+          const unsigned dl2 = (unsigned)dl * 0x10001u;
+#pragma unroll
+          for (int o = q; o < q + 4; o += 2) {
+            const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{sq[o - q], sq[o - q + 1]};
+            const f32x2 r = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              const float cc = r[h];
+              wv1[o + h] = vmed3(wv0[o + h], wv1[o + h], cc);  // second smallest
+              if (PKI) {
+                const unsigned hm = h ? 0xffff0000u : 0x0000ffffu;
+                wi0p[o >> 1] = cc < wv0[o + h] ? (wi0p[o >> 1] & ~hm) | (dl2 & hm) : wi0p[o >> 1];
+              } else {
+                wi0[o + h] = cc < wv0[o + h] ? dl : wi0[o + h];
+              }
+              wv0[o + h] = vmin(wv0[o + h], cc);
+            }
+          }
+        }
       }
+      return;
     }
 #pragma unroll
     for (int j = 0; j < DPW; j++) {
       const int dl = c * DC + wave + NW * j;
       if (dl >= a.D) break;
-      if (FUSE) {
-#pragma unroll
-        for (int o = 0; o < TH; o += 2) {
-          const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{srv[o], srv[o + 1]};
-          const f32x2 r = f32x2{1.0f, 1.0f} - f32x2{vmax(e.x, -1.0f), vmax(e.y, -1.0f)};
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const float cc = r[h];
-            wv1[o + h] = vmed3(wv0[o + h], wv1[o + h], cc);  // second smallest
-            wi0[o + h] = cc < wv0[o + h] ? dl : wi0[o + h];
-            wv0[o + h] = vmin(wv0[o + h], cc);
-          }
-        }
-        continue;
-      }
       // buffer stores: the level plane as a buffer resource (scalar), the lane's
       // byte offset fixed for the tile, the row offset scalar -- no address VALU
       const __amdgpu_buffer_rsrc_t rs =
@@ -426,7 +458,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
       for (int o = 0; o < TH; o += 2) {
         const f32x2 e = f32x2{E[j][o], E[j][o + 1]} * f32x2{sr[o], sr[o + 1]};
-        const f32x2 m = f32x2{vmax(e.x, -1.0f), vmax(e.y, -1.0f)};
+        const f32x2 m = f32x2{vmax_m1(e.x), vmax_m1(e.y)};
         const f32x2 r = f32x2{1.0f, 1.0f} - m;
         cst[o] = r.x;
         cst[o + 1] = r.y;
@@ -511,7 +543,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // peeled.  The others keep the flat loop: their second copy of the step
   // spilled at the 128-VGPR cap (fused K = 7 scratch 104 -> 532 bytes, K = 5
   // non-EVEN DPW 4 72 -> 452)
-  constexpr bool PEEL = K == 5 && EVEN;
+  constexpr bool PEEL = K == 5 && PAR == kParEven;
   auto step = [&](int t, int n, int cprev, auto first) {
     constexpr bool FIRST = decltype(first)::value;
     const int n1 = n + 1 == nn ? 0 : n + 1;
@@ -536,10 +568,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (int j = 0; j < DPW; j++) {
       const int colo = lvv[2 * j], rows = lvv[2 * j + 1];
       u32x2 pv[NR];
-      if (EVEN)
-        read_rows<NR, BW, true>(npk + colo + ln, rows & 0xffff, pv);
-      else
-        read_rows<NR, BW, false>(npk + colo + ln, rows & 0xffff, pv);
+      read_rows<NR, BW, PAR>(npk + colo + ln, rows & 0xffff, pv);
       // prefix sums over band rows of the horizontal K-tap centred correlation
       // prefix sums biased by kMagic: as floats they are 1.5 * 2^23 + the sum
       // (|sum| < 2^22), so a difference of two is the exact integer window sum
@@ -549,10 +578,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
       for (int k = 1; k < NR; k++) ps[k] = dot4(qlo[k], pv[k].x, dot4(qhi[k], pv[k].y, ps[k - 1]));
       f32x4 sv[TH / 2];
-      if (EVEN)
-        read_stat_pairs<TH, BW, true>(nst + colo + ln, rows >> 16, sv);
-      else
-        read_stat_pairs<TH, BW, false>(nst + colo + ln, rows >> 16, sv);
+      read_stat_pairs<TH, BW, PAR>(nst + colo + ln, rows >> 16, sv);
 #pragma unroll
       for (int m = 0; m < TH / 2; m++) {
         const int o = 2 * m;
@@ -597,6 +623,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     float* m0 = (float*)smem;
     float* m1 = m0 + NW * TP;
     int* mi = (int*)(m1 + NW * TP);
+    if (PKI)
+#pragma unroll
+      for (int o = 0; o < TH; o++) {
+        const unsigned v = (o & 1) ? wi0p[o >> 1] >> 16 : wi0p[o >> 1] & 0xffffu;
+        wi0[o] = v == 0xffffu ? -1 : (int)v;
+      }
     __syncthreads();
 #pragma unroll
     for (int o = 0; o < TH; o++) {
@@ -639,7 +671,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
 struct NccPlan {
   std::vector<int32_t> table;  // NccRec [nchunks][nn][NW waves] as int32
   int band_w = 0, pk_pairs = 0, st_pairs = 0;
-  bool even = true;  // every level's band rows start on a pair boundary
+  bool even = true;  // every level's band rows start on a pair boundary (kParEven)
+  bool odd = true;   // every pk start odd, every stats start even (kParOdd)
+  int par() const { return even ? kParEven : odd ? kParOdd : kParMixed; }
 };
 
 inline int floor_half(int v) { return v >> 1; }  // arithmetic: floor(v / 2)
@@ -677,13 +711,14 @@ NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const fl
           const int dl = c * DC + w + NW * j;
           if (dl >= D) {  // dummy level past the end: the band origin's even rows
             e[4 + 2 * j] = 0;
-            e[5 + 2 * j] = pr | (sr << 16);
+            e[5 + 2 * j] = pr | (sr << 16);  // same parity as the real levels'
             continue;
           }
           const int ty = ty_of(dl, n);
           e[4 + 2 * j] = txmax - tx_of(dl, n);
           e[5 + 2 * j] = (pr + tymax - ty) | ((sr + tymax - ty) << 16);
           if (((pr + tymax - ty) | (sr + tymax - ty)) & 1) p.even = false;
+          if (!((pr + tymax - ty) & 1) || ((sr + tymax - ty) & 1)) p.odd = false;
         }
       }
       spx = std::max(spx, txmax - txmin);
@@ -694,11 +729,11 @@ NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const fl
   return p;
 }
 
-template <int K, int TH, int DPW, int NW, int BW, bool EVEN>
+template <int K, int TH, int DPW, int NW, int BW, int PAR>
 int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
                   const WtaOut& wo, size_t lds) {
   hipStream_t s = ctx->stream;
-  const int variant[7] = {K, TH, DPW, NW, BW, EVEN ? 1 : 0, vol ? 0 : 1};
+  const int variant[7] = {K, TH, DPW, NW, BW, PAR, vol ? 0 : 1};
   std::copy(variant, variant + 7, ctx->ncc_last);
   constexpr int DC = NW * DPW;
   a.tiles_x = (a.W + 63) / 64;
@@ -706,7 +741,7 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
   a.tiles_per_xcd = (a.nref * a.ntiles + 7) / 8;
   a.nch = (a.D + DC - 1) / DC;
   dim3 g(8 * a.tiles_per_xcd);
-  auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, EVEN, false> : k_ncc_volume<K, TH, DPW, NW, BW, EVEN, true>;
+  auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, PAR, false> : k_ncc_volume<K, TH, DPW, NW, BW, PAR, true>;
   if (!vol) lds = std::max(lds, (size_t)3 * 4 * NW * TH * 64) + 4 * TH * 64;  // WTA partials; + s_r [64][TH]
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -788,32 +823,33 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
   return ok;
 }
 
+template <int K, int DPW, int NW, int PAR>
+int launch_bw(mvs_ctx* ctx, int bwt, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
+              const WtaOut& wo, size_t lds) {
+  if (bwt == 64) return launch_ncc_bw<K, 8, DPW, NW, 64, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 80) return launch_ncc_bw<K, 8, DPW, NW, 80, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 96) return launch_ncc_bw<K, 8, DPW, NW, 96, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
+  return launch_ncc_bw<K, 8, DPW, NW, 256, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
+}
+// the parity-specific kernels only where they occur: kParEven for K = 5
+// (horizontal bands, R = 2), kParOdd for K = 7 (R = 3)
 template <int K, int DPW, int NW>
-int launch_bw_even(mvs_ctx* ctx, int bwt, bool even, const uint2* stats, const uint2* pk, const NccRec* plan,
-                   NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
-  if (even && !ctx->ncc_general) {
-    if (bwt == 64) return launch_ncc_bw<K, 8, DPW, NW, 64, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-    if (bwt == 80) return launch_ncc_bw<K, 8, DPW, NW, 80, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-    if (bwt == 96) return launch_ncc_bw<K, 8, DPW, NW, 96, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-    if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-    if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-    return launch_ncc_bw<K, 8, DPW, NW, 256, true>(ctx, stats, pk, plan, a, vol, wo, lds);
-  }
-  if (bwt == 64) return launch_ncc_bw<K, 8, DPW, NW, 64, false>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 80) return launch_ncc_bw<K, 8, DPW, NW, 80, false>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 96) return launch_ncc_bw<K, 8, DPW, NW, 96, false>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, false>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, false>(ctx, stats, pk, plan, a, vol, wo, lds);
-  return launch_ncc_bw<K, 8, DPW, NW, 256, false>(ctx, stats, pk, plan, a, vol, wo, lds);
+int launch_bw_par(mvs_ctx* ctx, int bwt, int par, const uint2* stats, const uint2* pk, const NccRec* plan,
+                  NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
+  constexpr int KPAR = K == 5 ? kParEven : kParOdd;
+  if (par == KPAR && !ctx->ncc_general) return launch_bw<K, DPW, NW, KPAR>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);
+  return launch_bw<K, DPW, NW, kParMixed>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);
 }
 template <int K>
-int launch_variant(mvs_ctx* ctx, const NccChoice& c, int bwt, bool even, const uint2* stats, const uint2* pk,
+int launch_variant(mvs_ctx* ctx, const NccChoice& c, int bwt, int par, const uint2* stats, const uint2* pk,
                    const NccRec* plan, NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
-  if (c.dpw == 4 && c.nw == 8) return launch_bw_even<K, 4, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
-  if (c.dpw == 2 && c.nw == 8) return launch_bw_even<K, 2, 8>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
-  if (c.dpw == 4) return launch_bw_even<K, 4, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
-  if (c.dpw == 2) return launch_bw_even<K, 2, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
-  return launch_bw_even<K, 1, 4>(ctx, bwt, even, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 4 && c.nw == 8) return launch_bw_par<K, 4, 8>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 2 && c.nw == 8) return launch_bw_par<K, 2, 8>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 4) return launch_bw_par<K, 4, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 2) return launch_bw_par<K, 2, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
+  return launch_bw_par<K, 1, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
 }
 
 }  // namespace
@@ -837,7 +873,7 @@ int launch_box_stats(hipStream_t s, const uint8_t* l8, int V, int W, int H, int 
 // runs of consecutive views with the same (DPW, NW) whose merged bands still
 // fit every member's LDS cap share one launch (up to kMaxRef views, fused
 // sweep only: a cost volume holds one view), with the widest band stride and
-// EVEN only when every member's rows start on pairs -- the same arithmetic,
+// a parity-specific kernel only when every member has that parity -- the same arithmetic,
 // one kernel boundary (~11 us between two of these launches) per run.
 int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const float* levels_host, int D,
                     const int* vs_host, const int* sn_host, int aw, float bl, int K, int z0, int z1, float* vol,
@@ -846,6 +882,7 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   if (vol && z1 - z0 != 1) return arg_fail("the NCC cost volume holds one reference view");
   if (W < 2) return arg_fail("NCC sweep needs W >= 2");
   if (K != 5 && K != 7) return arg_fail("NCC window must be 5 or 7");
+  if (!vol && D > 65535) return arg_fail("fused NCC sweep: at most 65535 levels");  // K = 7 packs levels in 16 bits
   const int n = z1 - z0;
   if (n <= 0) return 0;
   std::vector<NccChoice> ch(n);
@@ -875,7 +912,7 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   const int maxrun = re ? std::max(1, std::min(kMaxRef, atoi(re))) : kMaxRef;
   for (int i = 0; i < n;) {
     int bwt = ch[i].bwt, pkp = ch[i].plan.pk_pairs, stp = ch[i].plan.st_pairs;
-    bool even = ch[i].plan.even;
+    int par = ch[i].plan.par();
     size_t cap = ch[i].cap;
     int j = i + 1;
     while (!vol && j < n && j - i < maxrun && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw) {
@@ -887,7 +924,7 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
       pkp = p2;
       stp = s2;
       cap = c2;
-      even = even && ch[j].plan.even;
+      if (ch[j].plan.par() != par) par = kParMixed;
       j++;
     }
     NccArgs a{};
@@ -911,8 +948,8 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
     if (rc) return rc;
     const WtaOut wo{levels_dev, disp ? disp + P * i : nullptr, conf ? conf + P * i : nullptr};
     const size_t lds = 2 * 16 * (size_t)(pkp + stp) * bwt;
-    rc = K == 5 ? launch_variant<5>(ctx, ch[i], bwt, even, stats, pk, (const NccRec*)dev, a, vol, wo, lds)
-                : launch_variant<7>(ctx, ch[i], bwt, even, stats, pk, (const NccRec*)dev, a, vol, wo, lds);
+    rc = K == 5 ? launch_variant<5>(ctx, ch[i], bwt, par, stats, pk, (const NccRec*)dev, a, vol, wo, lds)
+                : launch_variant<7>(ctx, ch[i], bwt, par, stats, pk, (const NccRec*)dev, a, vol, wo, lds);
     if (rc) return rc;
     i = j;
   }

@@ -197,9 +197,10 @@ def test_every_ncc_variant(eng, K, geom):
                 same(fc, oc, f"fused conf {tag}")
     # every pitch from the narrowest the geometry allows (4-level chunks) up
     assert seen == {b for b in _BANDS if b >= {"horizontal": 80, "vertical": 80, "vertical_only": 64}[geom]}, seen
-    # K = 5 horizontal bands start on a row pair (R + tymax even); K = 7 (R = 3)
-    # and fractional vertical shifts start on odd rows
-    assert evens == ({0, 1} if geom == "horizontal" and K == 5 else {0})
+    # row-parity mode (kParMixed 0 / kParEven 1 / kParOdd 2): K = 5 horizontal
+    # bands start on a row pair (R + tymax even), K = 7 (R = 3) horizontal
+    # bands on an odd row; fractional vertical shifts mix both
+    assert evens == ({0, 1 if K == 5 else 2} if geom == "horizontal" else {0})
 
 
 @pytest.mark.parametrize("case", ["c2_like", "c4_like", "c5_like", "frac_vertical", "forced"])

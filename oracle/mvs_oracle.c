@@ -1,13 +1,17 @@
 /* ORACLE TEST INFRASTRUCTURE -- CPU restatement of the reference hot path.
  *
- * PARITY UNPINNED: the reference (clMVDE/clcode.cl, OpenCL C) ships no tests,
- * fixtures or golden vectors, and running its kernels (on the GPU box through
- * the ROCm OpenCL runtime) was denied for this build; a CPU build would need a
- * stand-in OpenCL runtime the image lacks.  This file restates the kernels'
- * arithmetic from the reference source text, statement by statement, under the
- * numerical definition in include/mvs_detmath.h (IEEE ops, no contraction,
- * pinned builtins).  Only tests/, __graft_entry__.smoke() and bench.py's
- * cpu_baseline leg may call it, and only as the checker / CPU baseline.
+ * PINNED BY THE REFERENCE'S KEPT OUTPUTS: the reference (clMVDE/clcode.cl,
+ * OpenCL C) ships no tests, fixtures or golden vectors, and running its kernels
+ * (on the GPU box through the ROCm OpenCL runtime) was denied for this build; a
+ * CPU build would need a stand-in OpenCL runtime the image lacks.  This file
+ * restates the kernels' arithmetic from the reference source text, statement by
+ * statement, under the numerical definition in include/mvs_detmath.h (IEEE
+ * ops, no contraction, pinned builtins), and is checked against the PNGs the
+ * reference keeps from its own runs (tests/ref_artifacts.py, DESIGN.md 0: SLIC
+ * overlays on 99.9994 % of the boundary pixels, seeds 99.886 %, six frozen
+ * crops bit-exact in tests/golden/ref_overlay_crops.npz).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may call it, and
+ * only as the checker / CPU baseline.
  *
  * Layouts are the reference's: rgbx [H][W][4] u8 (s0=R),
  * lab [H][W][4] f32, spixl [mh][mw][8] f32, labels [H][W] u32,

@@ -275,13 +275,194 @@ def score_flatness(quick):
     return out
 
 
+# ---------------------------------------------------------------------------
+# Refinement sensitivity (round 4): how far does each implementation-defined
+# choice move the refinement, against how far the reference's own plots sit?
+PROBE_BUILDS = {  # oracle/Makefile `probes`, MVS_PROBE_* in oracle/mvs_oracle.c
+    "rcpdiv": "every fp32 quotient of the refinement as a * RN(1/b)",
+    "libmexp": "glibc exp/expf in place of mvs_detmath",
+    "expulp1": "every expf result moved by a hash-chosen -1..+1 ulp",
+    "expulp2": "every expf result moved by a hash-chosen -2..+2 ulp",
+    "sqrtrsq": "sqrt(s) as s * RN(1/sqrt(s))",
+    "rcontract": "mul+add contracted (FMA) in the refinement only",
+    "rsys": "the systematic alternatives together: rcpdiv + libmexp + sqrtrsq + rcontract",
+    "rall": "all of the above together (ulp 1)",
+}
+
+
+def perturb_labels(labels, n, seed):
+    """Flip n interior boundary pixels of one view to the label of a 4-neighbour
+    that differs (the size of the reference's residual SLIC disagreement)."""
+    rng = np.random.default_rng(seed)
+    lb = labels.copy()
+    m = boundary_mask(lb)
+    ys, xs = np.nonzero(m)
+    pick = rng.choice(len(ys), size=min(n, len(ys)), replace=False)
+    for y, x in zip(ys[pick], xs[pick]):
+        nb = [lb[y + dy, x + dx] for dy, dx in ((0, 1), (0, -1), (1, 0), (-1, 0)) if lb[y + dy, x + dx] != lb[y, x]]
+        if nb:
+            lb[y, x] = nb[rng.integers(len(nb))]
+    return lb
+
+
+def refine_plots(sp, lb, rep, b):
+    st = b["st"]
+    r = orc.refine(sp, lb, rep, b["vs"], b["sn"], st.array_width, st.bl_ratio, st.spixl_size, st.gamma, st.alpha,
+                   st.fuse, st.kernel_step, st.kernel_size, st.no_prop)
+    it4 = np.stack([plot8(per_pixel(r["states"][4][k][..., 0], lb[k])) for k in range(9)])
+    fus = np.stack([plot8(r["disp"][k]) for k in range(9)])
+    return it4, fus
+
+
+def score_probes(label_flips=46):
+    """Started from the reference's seeds (read back from initD_dev<k>), the
+    refinement of every probe build and of label-perturbed inputs, each scored
+    against the reference's plots (7- propagate iteration 4, 8- Fusion fus4)
+    and against the pinned oracle's own plots; plus where the pinned oracle's
+    fus4 disagreement with the reference lies, bucketed by the distance to the
+    nearest pixel where its SLIC boundary differs from the reference's
+    (slic output/green<k>.png, the search-1 overlay family)."""
+    from scipy import ndimage
+    for name in PROBE_BUILDS:
+        BUILDS[name] = os.path.join(ROOT, "oracle", "_build", f"liboracle_{name}.so")
+        if not os.path.exists(BUILDS[name]):
+            os.system(f"make -s -C {os.path.join(ROOT, 'oracle')} probes")
+    b = beer_garden_stack(1)
+    ref_sp, _ = reference_seeds(b["spixl"], b["labels"])
+    ref_it4 = np.stack([load_gray(f"results/7- propagate/change6_alter1 {k}.png") for k in range(9)])
+    ref_fus = np.stack([load_gray(f"results/8- Fusion/fus4 {k}.png") for k in range(9)])
+    out = {"start": "the reference's seeds on the pinned oracle's search-1 labels", "variants": {}}
+
+    def record(name, what, it4, fus, base=None):
+        e = {"what": what, "iter4_vs_reference": float((it4 == ref_it4).mean()),
+             "fus4_vs_reference": float((fus == ref_fus).mean())}
+        if base is not None:
+            e["iter4_vs_pinned"] = float((it4 == base[0]).mean())
+            e["fus4_vs_pinned"] = float((fus == base[1]).mean())
+        out["variants"][name] = e
+        print(f"[probe] {name:12s} ref: it4 {e['iter4_vs_reference']:.4f} fus4 {e['fus4_vs_reference']:.4f}"
+              + (f"   pinned: it4 {e['iter4_vs_pinned']:.4f} fus4 {e['fus4_vs_pinned']:.4f}" if base else ""),
+              flush=True)
+
+    t0 = time.time()
+    use("pinned")
+    base = refine_plots(ref_sp, b["labels"], b["rep"], b)
+    record("pinned", "the pinned definition", *base)
+    out["seconds_per_refinement"] = time.time() - t0
+    for name, what in PROBE_BUILDS.items():
+        use(name)
+        record(name, what, *refine_plots(ref_sp, b["labels"], b["rep"], b), base=base)
+    # (d) labels perturbed at label_flips boundary pixels per view (~the
+    # reference's 412 SLIC residual pixels over the 9 views).  The superpixel
+    # records stay: SLIC's last step is an assignment, so the centres and
+    # colours the refinement reads are the previous labels' means (re-averaging
+    # them from the final labels moves every superpixel, not a few).  The
+    # extents are recomputed from the perturbed labels.
+    S = b["st"].spixl_size
+    for build in ("pinned", "rall"):
+        for seed in (1, 2):
+            use("pinned")
+            lbp = np.stack([perturb_labels(b["labels"][k], label_flips, 1000 * seed + k) for k in range(9)])
+            repp = orc.boundary(ref_sp, lbp, S)
+            use(build)
+            record(f"labels{seed}" + ("" if build == "pinned" else "+rall"),
+                   f"{label_flips} boundary pixels per view flipped (seed {seed})"
+                   + ("" if build == "pinned" else "; " + PROBE_BUILDS["rall"]),
+                   *refine_plots(ref_sp, lbp, repp, b), base=base)
+    use("pinned")
+    # where the pinned oracle leaves the reference's fus4 plot
+    ref_mask = np.stack([overlay_mask(load_rgb(f"results/slic output/green{k}.png"), load_rgb(BEER[k]))
+                         for k in range(9)])
+    ours = np.stack([boundary_mask(b["labels"][k]) for k in range(9)])
+    edges = [0, 4, 16, 64, 256, 1 << 30]
+    hist = {f"{lo}-{hi}" if hi < 1 << 30 else f">={lo}": [0, 0] for lo, hi in zip(edges, edges[1:])}
+    sp_dis = []
+    for k in range(9):
+        mism = np.zeros(ours[k].shape, bool)
+        mism[INNER] = ours[k][INNER] != ref_mask[k][INNER]
+        dist = ndimage.distance_transform_edt(~mism) if mism.any() else np.full(mism.shape, np.inf)
+        bad = base[1][k] != ref_fus[k]
+        for (lo, hi), key in zip(zip(edges, edges[1:]), hist):
+            sel = (dist >= lo) & (dist < hi)
+            hist[key][0] += int(sel.sum())
+            hist[key][1] += int((bad & sel).sum())
+        lbk = b["labels"][k].astype(np.int64)
+        n_sp = int(lbk.max()) + 1
+        bad_sp = np.bincount(lbk.ravel(), weights=bad.ravel(), minlength=n_sp)
+        tot_sp = np.bincount(lbk.ravel(), minlength=n_sp)
+        sp_dis.append(((bad_sp > 0).sum(), (bad_sp >= 0.5 * np.maximum(tot_sp, 1)).sum(), (tot_sp > 0).sum()))
+    out["fus4_disagreement_by_distance_to_slic_mismatch"] = {
+        k: {"pixels": v[0], "disagreeing": v[1], "frac": v[1] / max(v[0], 1)} for k, v in hist.items()}
+    sp_dis = np.array(sp_dis).sum(0)
+    out["fus4_disagreement_superpixels"] = {"any_pixel": int(sp_dis[0]), "majority": int(sp_dis[1]),
+                                           "superpixels": int(sp_dis[2])}
+    print("[probe] disagreement by distance to a SLIC mismatch:",
+          {k: round(v["frac"], 4) for k, v in out["fus4_disagreement_by_distance_to_slic_mismatch"].items()})
+    return out
+
+
+STAGE_PLOTS = {  # the per-superpixel stage plots of the 15-view c<k>f1 array
+    "flatness_new": "results/2- flatness/flatness_new {k}.png",
+    "initSm_dev": "results/3- initialize smoothness/initSm_dev {k}.png",
+    "initCs_dev": "results/4- initialize consistency/initCs_dev {k}.png",
+}
+
+
+def score_stage_purity():
+    """Whether the flatness / init-smoothness / init-consistency plots come
+    from the same SLIC labels as the oracle's: each plot is a per-superpixel
+    value painted over the superpixel's pixels (depth_refinement.cpp:299-322,
+    390-391), so on the labels that made it the plot is constant on every
+    superpixel (purity 1.0, as the seed plots are on the oracle's labels:
+    99.9986 %).  A purity well below 1 on the oracle's labels (both
+    candidate searches) means another run's segmentation, so these plots
+    cannot pin the oracle's flatness / init stages."""
+    out = {}
+    for fam, pat in STAGE_PLOTS.items():
+        row = {}
+        for search in (0, 1):
+            pur = []
+            for k in range(15):
+                _, _, lb = orc.slic(rgbx_of(load_rgb(C_SCENE[k])), 8, search=search)
+                pur.append(purity(lb, load_gray(pat.format(k=k))))
+            row[f"search{search}"] = {"purity": float(np.mean(pur)), "per_view": pur}
+        out[fam] = row
+        print(f"[purity] {fam}: search 0 {row['search0']['purity']:.4f}, search 1 {row['search1']['purity']:.4f}",
+              flush=True)
+    # the reference: the seed plots of the Beer-Garden array on the oracle's labels
+    b = beer_garden_stack(1)
+    pur = [purity(b["labels"][k], load_gray(f"results/1- initialize disparity/initD_dev{k}.png")) for k in range(9)]
+    out["initD_dev (Beer-Garden, control)"] = {"search1": {"purity": float(np.mean(pur)), "per_view": pur}}
+    print(f"[purity] control initD_dev: {np.mean(pur):.6f}", flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--purity", action="store_true",
+                    help="only the stage-plot purity check (profiles/r04/ref_stage_purity.json)")
     ap.add_argument("--quick", action="store_true", help="fewer views and settings (about a minute)")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03_ref_artifacts.json"))
+    ap.add_argument("--probes", action="store_true",
+                    help="only the refinement sensitivity table (profiles/r04/ref_probes.json)")
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
     if not os.path.isdir(REF):
         sys.exit("ref_artifacts: /root/reference is absent (container-only script)")
+    if a.purity:
+        res = score_stage_purity()
+        out = a.out or os.path.join(ROOT, "profiles", "r04", "ref_stage_purity.json")
+        with open(out, "w") as f:
+            json.dump(res, f, indent=1)
+        print("wrote", out)
+        return
+    if a.probes:
+        res = score_probes()
+        out = a.out or os.path.join(ROOT, "profiles", "r04", "ref_probes.json")
+        with open(out, "w") as f:
+            json.dump(res, f, indent=1)
+        print("wrote", out)
+        return
+    a.out = a.out or os.path.join(ROOT, "profiles", "r03_ref_artifacts.json")
     for b, path in BUILDS.items():
         if not os.path.exists(path):
             os.system(f"make -s -C {os.path.join(ROOT, 'oracle')} {'all' if b == 'pinned' else b}")

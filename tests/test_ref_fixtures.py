@@ -70,6 +70,47 @@ def test_gpu_reproduces_reference_overlays(engine):
         check(mask_of(lb.cpu().numpy()[0].view(np.uint32)), want, meta, src)
 
 
+# ---- the residual, asserted (tests/golden/gen_ref_crops.py --residual) --------
+# Two crops centred on the densest clusters of the oracle's SLIC residual
+# against green_new0 / green_new4: the masks differ from the reference's on an
+# exact, recorded number of interior pixels (the reference device's
+# implementation-defined powr / divide), and the GPU leaves the same pixels.
+RESID = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_overlay_residual.npz")
+
+
+def residual_crops():
+    with np.load(RESID, allow_pickle=False) as z:
+        return [(z[f"rgb{i}"], z[f"mask{i}"], z[f"meta{i}"], str(z[f"src{i}"])) for i in range(int(z["n"]))]
+
+
+def residual(mask_full, want, meta):
+    mg = int(meta[3])
+    got = mask_full[mg:mask_full.shape[0] - mg, mg:mask_full.shape[1] - mg]
+    return got != want
+
+
+@pytest.mark.parametrize("i", range(2))
+def test_oracle_residual_crop(i):
+    rgb, want, meta, src = residual_crops()[i]
+    _, _, lb = orc.slic(rgbx(rgb), 8, 0.6, 5, search=int(meta[0]))
+    bad = int(np.count_nonzero(residual(mask_of(lb), want, meta)))
+    assert bad == int(meta[4]) > 0, f"{src}: {bad} residual pixels, recorded {int(meta[4])}"
+
+
+@pytest.mark.gpu
+def test_gpu_residual_crops(engine):
+    import torch
+    for rgb, want, meta, src in residual_crops():
+        _, _, olb = orc.slic(rgbx(rgb), 8, 0.6, 5, search=int(meta[0]))
+        img = torch.from_numpy(rgbx(rgb)[None]).cuda()
+        lab, _ = engine.cvt(img)
+        _, lb = engine.slic(lab, 8, 0.6, 5, search=int(meta[0]))
+        glb = lb.cpu().numpy()[0].view(np.uint32)
+        assert np.array_equal(glb, olb), f"{src}: GPU labels differ from the oracle's"
+        r = residual(mask_of(glb), want, meta)
+        assert int(np.count_nonzero(r)) == int(meta[4]) > 0, src
+
+
 # ---- full images, container only ---------------------------------------------
 needs_ref = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "results")), reason="reference tree absent")
 

@@ -383,9 +383,9 @@ def bench(args, world, rank, local):
     # the fused NCC headline runs the superpixel chain (SLIC, extents,
     # superpixel sweep) on a side stream beside the per-pixel chain
     # (pipeline.py, concurrent=True): C2 2.55 -> 2.52 ms per step in three
-    # interleaved rounds (profiles/r03j_concurrent.txt); --serial turns it off
+    # interleaved rounds (profiles/archive/r03j_concurrent.txt); --serial turns it off
     # (c3, with refinement and the filter after the join: 3.462-3.469 ->
-    # 3.431-3.434 ms in three interleaved rounds, profiles/r03n_ref_c3.txt)
+    # 3.431-3.434 ms in three interleaved rounds, profiles/archive/r03n_ref_c3.txt)
     conc_head = args.concurrent or (fused and not sharded and cost == "ncc" and not args.serial)
 
     def make(fz, conc=False):

@@ -16,7 +16,7 @@ CONFIG=c2 ARGS="--cost sad --steps 5 --warmup 2 --no-reference-cost" bash script
 CONFIG=c2 TAG=r03g_c2sad BENCH_ARGS="--cost sad --steps 3 --warmup 1 --no-cpu-baseline --no-sharded --no-reference-cost" \
   bash scripts/profile.sh || exit 1
 mkdir -p gpurun_out/r03g/prof_sad && mv profiles/pmc_wta_c2.json gpurun_out/r03g/prof_sad/ 2>/dev/null; mv profiles/pmc_ncc_c2.json gpurun_out/r03g/prof_sad/ 2>/dev/null
-cp profiles/r03g_c2sad_* gpurun_out/r03g/prof_sad/ 2>/dev/null
+cp profiles/archive/r03g_c2sad_* gpurun_out/r03g/prof_sad/ 2>/dev/null
 CONFIG=c5 TAG=r03g_c5 BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-sharded --no-reference-cost" bash scripts/profile.sh || exit 1
-mkdir -p gpurun_out/r03g/prof_c5 && cp profiles/r03g_c5_* profiles/pmc_wta_c5.json profiles/pmc_ncc_c5.json gpurun_out/r03g/prof_c5/ 2>/dev/null
+mkdir -p gpurun_out/r03g/prof_c5 && cp profiles/archive/r03g_c5_* profiles/pmc_wta_c5.json profiles/pmc_ncc_c5.json gpurun_out/r03g/prof_c5/ 2>/dev/null
 echo all done

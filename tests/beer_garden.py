@@ -17,7 +17,7 @@ Three steps (this is checker infrastructure under tests/, not a pytest module):
 
 data/ is listed in .gpurunignore (it is 30 MB and only this script reads it):
 take that line out for the `gpu` step.  The GPU step writes gpurun_out/beer/{result.json, fus <k>.png, init <k>.png};
-`compare` writes profiles/r02_beer_garden.json.  data/ is git-ignored: the
+`compare` writes profiles/archive/r02_beer_garden.json.  data/ is git-ignored: the
 images are the reference's input data, not part of this repository's history.
 """
 from __future__ import annotations

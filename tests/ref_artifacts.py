@@ -8,7 +8,7 @@ This script re-renders each family the way the reference's writer does, from
 the oracle's output on the same decoded pixels, and scores the agreement over
 a documented grid of settings.  CPU only, container only (the reference tree
 does not exist on the GPU box); it lives under tests/ because it loads the
-oracle.  Writes profiles/r03_ref_artifacts.json.
+oracle.  Writes profiles/archive/r03_ref_artifacts.json.
 
 Renderers (reference file:line):
   * SLIC overlay  -- clSLIC::draw_segmentation_lines, clSLIC.cpp:447-478: an

@@ -11,7 +11,7 @@ oracle generated itself).
   oracle's S = 8 overlays against results/slic output/green_new<k>.png and its
   superpixel seeds against results/1- initialize disparity/initD_dev<k>.png
   (the whole 9-view Beer-Garden array); DESIGN.md section 0 and
-  profiles/r03_ref_artifacts.json give the scores.
+  profiles/archive/r03_ref_artifacts.json give the scores.
 """
 from __future__ import annotations
 
@@ -122,7 +122,7 @@ def test_full_overlay_green_new0():
     ref = overlay_mask(load_rgb("results/slic output/green_new0.png"), rgb)
     _, _, lb = orc.slic(rgbx_of(rgb), 8)
     bad = int(np.count_nonzero(boundary_mask(lb)[INNER] != ref[INNER]))
-    assert bad <= 9, bad  # 9 of 2,067,604 (profiles/r03_ref_artifacts.json)
+    assert bad <= 9, bad  # 9 of 2,067,604 (profiles/archive/r03_ref_artifacts.json)
 
 
 @needs_ref

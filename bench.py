@@ -473,6 +473,16 @@ def bench(args, world, rank, local):
                 "valu_issue_frac": round(per_view["insts"] * vpc / t_f / VALU_PEAK, 4),
                 "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op",
                 "valu_source": per_view["source"]})
+            # the roofline of the kernel the headline step actually spends its time in
+            ach = per_view["insts"] * vpc / t_f / 1e9
+            res["roofline_headline"] = {
+                "bound": "valu", "kernel": "k_ncc_volume<..., FUSE=true> (fused sweep + WTA)",
+                "achieved": round(ach, 1), "peak": round(VALU_PEAK / 1e9, 1), "unit": "G VALU wave-instr/s",
+                "frac": round(ach * 1e9 / VALU_PEAK, 4),
+                "algorithmic": f"{round(per_view['insts'])} VALU wave-instructions per reference view "
+                               f"(SQ_INSTS_VALU of its own PMC pass, {per_view['source']}) over the HIP-event "
+                               f"time per view of the serial pass",
+                "avg_ms_per_view": round(t_f * 1e3 / vpc, 4)}
 
     # the two-pass step (cost volume in HBM + k_wta), same protocol: the
     # north star's roofline is k_wta's read of that volume

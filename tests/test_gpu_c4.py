@@ -3,7 +3,9 @@ reference with its 5 nearest neighbours (params.nearest_neighbours), through
 the view-sharded pipeline on the HIP backend -- SLIC, extents, superpixel
 sweep, fused NCC 5x5 sweep + WTA over 128 levels, refinement (5 propagations,
 compute_consistency over the 5-NN lists, clcode.cl:1528-1631) and the
-cross-view filter -- on a 256 x 128 crop with S = 16.
+cross-view filter -- on a 256 x 128 crop with S = 16 and on a 384 x 192 crop
+with C4's own S = 32 (the tile-fused SLIC path, k_assign_tiles +
+k_update_finalize, that the full-size C4 run takes).
 
 * world 1: the product orchestration (ViewGather) on one GPU;
 * world 8: each rank r of a world of 8 runs ShardedPipeline with a replay of
@@ -25,10 +27,12 @@ from cl_multiview_stereo_amd.engine import CameraArray
 from oracle import oracle as orc
 from tests.replay_gather import RecordingGather, ReplayGather
 
-AW, AH, W, H, S, DMAX = 8, 4, 256, 128, 16, 127
+AW, AH, DMAX = 8, 4, 127
+GEOMS = {"s16": (256, 128, 16), "s32": (384, 192, 32)}  # crop W, H and superpixel size S
 
 
-def _case():
+def _case(geom="s16"):
+    W, H, S = GEOMS[geom]
     # a scene 0..15 px deep, swept over 128 hypotheses (C4's 0..127 levels)
     stack, _ = synth.make_stack(W, H, AW, AH, 0, 15, 1.0, 0xC4)
     levels = params.disparity_levels(0, DMAX, 1)
@@ -41,10 +45,11 @@ def _case():
 _ORACLE = {}
 
 
-def _oracle():
-    if _ORACLE:
-        return _ORACLE
-    stack, levels, vs, sn, st = _case()
+def _oracle(geom="s16"):
+    if geom in _ORACLE:
+        return _ORACLE[geom]
+    stack, levels, vs, sn, st = _case(geom)
+    S = st.spixl_size
     V = AW * AH
     outs = [orc.slic(stack[v], S) for v in range(V)]
     lab = np.stack([o[0] for o in outs])
@@ -56,8 +61,8 @@ def _oracle():
     disp = np.stack([orc.wta(orc.ncc_volume(q, levels, vs, sn, AW, 1.0, 5, z), levels)[0] for z in range(V)])
     ref = orc.refine(sp, lb, rep, vs, sn, AW, 1.0, S)  # main()'s refinement settings
     _, filt = orc.filt(ref["disp"], AW, 1.0, 1.0)
-    _ORACLE.update(labels=lb, spixl=sp, disp=disp, refined=ref["disp"], filt=filt)
-    return _ORACLE
+    _ORACLE[geom] = dict(labels=lb, spixl=sp, disp=disp, refined=ref["disp"], filt=filt)
+    return _ORACLE[geom]
 
 
 def _bits(t):
@@ -74,9 +79,10 @@ def _check(out, want, z0, z1):
 
 
 @pytest.mark.gpu
-def test_c4_world1_matches_oracle(engine):
-    stack, levels, vs, sn, st = _case()
-    want = _oracle()
+@pytest.mark.parametrize("geom", sorted(GEOMS))
+def test_c4_world1_matches_oracle(engine, geom):
+    stack, levels, vs, sn, st = _case(geom)
+    want = _oracle(geom)
     cam = CameraArray(AW, 1.0, levels, vs, sn)
     pipe = ShardedPipeline(EngineBackend(engine, fused=True), st, cam, ViewGather(AW * AH), pixel_cost="ncc",
                            refine=True, filt=True)
@@ -85,13 +91,13 @@ def test_c4_world1_matches_oracle(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shard", ["rows", "views"])
-def test_c4_world8_replay_matches_oracle(engine, shard):
+@pytest.mark.parametrize("shard,geom", [("rows", "s16"), ("views", "s16"), ("rows", "s32")])
+def test_c4_world8_replay_matches_oracle(engine, shard, geom):
     """shard: the filter sharded by image rows (the default: every reference
     view's rows of the rank's band, then the rows -> views exchange) or by
     reference view (row-banded proj all-gather)."""
-    stack, levels, vs, sn, st = _case()
-    want = _oracle()
+    stack, levels, vs, sn, st = _case(geom)
+    want = _oracle(geom)
     V = AW * AH
     cam = CameraArray(AW, 1.0, levels, vs, sn)
     be = EngineBackend(engine, fused=True)

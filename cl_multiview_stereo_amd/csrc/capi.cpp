@@ -406,9 +406,11 @@ static int propagate(mvs_ctx* c, int W, int H, int S, const float* spixl, const 
     return mvs::arg_fail((std::string(fn) + ": bad arguments").c_str());
   RC(upload_meta(c, a));
   if (z0 < 0 || z1 > a->view_count || z0 > z1) return mvs::arg_fail((std::string(fn) + ": bad view range").c_str());
+  int max_nbr = 0;
+  for (int z = z0; z < z1; z++) max_nbr = std::max(max_nbr, (int)a->subset_num[z]);
   return mvs::launch_propagate(c->stream, a->view_count, W, H, S, a->array_width, a->bl_ratio, spixl, labels, lbits,
                                rep, flat, c->d_vs, c->d_sn, iter, alpha, gamma, fuse, kernel_steps, kss, st_in,
-                               st_out, z0, z1);
+                               st_out, z0, z1, max_nbr);
 }
 
 int mvs_propagate_d(mvs_ctx* c, int W, int H, int S, const float* spixl, const uint32_t* labels, const uint8_t* rep,

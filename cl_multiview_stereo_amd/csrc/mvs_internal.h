@@ -104,7 +104,8 @@ int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float b
 int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
                      const void* labels, int lbits, const uint8_t* rep, const float* flat, const int* vs,
                      const int* sn, int iter, float alpha, float gamma, float fuse, int nks, float kss,
-                     const float* st_in, float* st_out, int z0, int z1);
+                     const float* st_in, float* st_out, int z0, int z1,
+                     int max_nbr);  // the largest neighbour count of views [z0, z1)
 int launch_spixl_to_image(hipStream_t s, int V, int W, int H, int S, const float* spixl,
                           const void* labels, int lbits, const float* state, float* disp);
 int launch_filter(hipStream_t s, int V, int W, int H, int aw, float bl, float fuse, const float* full,

@@ -460,7 +460,12 @@ __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
-template <typename LT>
+// FAST: the host knows every superpixel of the launch takes the lane-parallel
+// path (nks <= 13, so 9 + 4 nks <= 64 smoothness terms, and every view of
+// [z0, z1) has <= kTriViews neighbours): the one-lane-per-candidate fallback is
+// not compiled in, and its unrolled 9-sample consistency arrays no longer set
+// the register allocation of the path that runs (reference defaults, C3, C4)
+template <typename LT, bool FAST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_propagate(RArgs c, const float* __restrict__ spixl,
                                                    const void* __restrict__ labels,
                                                    const uint8_t* __restrict__ rep, const float2* __restrict__ flat,
@@ -491,7 +496,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   // neighbour centres.  Sums keep the reference's term order.
   const int ss = step_size_of(p.fl.x, kss);
   const int nterm = 9 + 4 * nks;
-  const bool fast_sm = nterm <= 64;
+  const bool fast_sm = FAST || nterm <= 64;
   float t_simi = 0.f, t_sx = 0.f, t_sy = 0.f, t_sd = 0.f, wn = 0.f;
   unsigned long long t_valid = 0ull;
   if (fast_sm) {
@@ -553,7 +558,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   };
   const int nslot = 9 + 4 * nks;
   const int nv = sn[z];
-  if (fast_sm && nv <= kTriViews) {
+  if (FAST || (fast_sm && nv <= kTriViews)) {
     // Lane-parallel evaluation in groups of 8 candidates: lane 8t + r works
     // for candidate t of the group (L lanes per candidate in general: 8, or
     // more for a partial last group, see below).  The smoothness products simi_l * exp(...)
@@ -718,7 +723,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
       }
     }
-  } else {
+  } else if (!FAST) {
     // one lane per plane candidate, in batches of 64
     for (int b = 0; b < nslot; b += 64) {
       const int k = b + lane;
@@ -1385,11 +1390,14 @@ int launch_init_state(hipStream_t s, int V, int W, int H, int S, int aw, float b
 int launch_propagate(hipStream_t s, int V, int W, int H, int S, int aw, float bl, const float* spixl,
                      const void* labels, int lbits, const uint8_t* rep, const float* flat, const int* vs,
                      const int* sn, int iter, float alpha, float gamma, float fuse, int nks, float kss,
-                     const float* st_in, float* st_out, int z0, int z1) {
+                     const float* st_in, float* st_out, int z0, int z1, int max_nbr) {
   if (z1 <= z0) return 0;
   RArgs c{V, W, H, S, map_dim(W, S), map_dim(H, S), aw, bl, fuse, alpha, gamma};
   const long nsp = (long)c.mw * c.mh * (z1 - z0);
-  hipLaunchKernelGGL(lbits == 16 ? k_propagate<uint16_t> : k_propagate<uint32_t>, dim3((unsigned)((nsp + 3) / 4)), dim3(256), 0, s, c, spixl, labels, rep,
+  const bool fast = nks <= 13 && max_nbr <= kTriViews;  // see k_propagate's FAST
+  auto kern = lbits == 16 ? (fast ? k_propagate<uint16_t, true> : k_propagate<uint16_t, false>)
+                          : (fast ? k_propagate<uint32_t, true> : k_propagate<uint32_t, false>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)((nsp + 3) / 4)), dim3(256), 0, s, c, spixl, labels, rep,
                      (const float2*)flat, vs, sn, iter, nks, kss, st_in, st_out, z0, nsp);
   MVS_LAUNCH_CHECK("k_propagate");
   return 0;

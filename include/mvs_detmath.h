@@ -91,9 +91,8 @@ MVS_HD double mvs_log(double x) {
  * Cody-Waite with fma, degree-7 Taylor by fma Horner, exact scaling.  Results
  * stay normal: x < -86.5 gives 0, x > ln(FLT_MAX) gives +inf.  <= 2 ulp. */
 MVS_HD float mvs_expf(float x) {
-  if (x != x) return x;
-  if (x > 88.72283935546875f) return 1.0f / 0.0f;
-  if (x < -86.5f) return 0.0f;
+  /* one range test on the common path (a NaN fails it); the rare cases after */
+  if (!(x >= -86.5f && x <= 88.72283935546875f)) return x != x ? x : (x > 0.0f ? 1.0f / 0.0f : 0.0f);
   const float log2e = 1.44269502162933349609375f;
   const float ln2_hi = 0.693147182464599609375f;   /* (float) ln 2 */
   const float ln2_lo = -1.904654323148236e-09f;    /* ln 2 - ln2_hi */

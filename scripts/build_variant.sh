@@ -10,7 +10,10 @@ mkdir -p $T/cl_multiview_stereo_amd/host $T/include $T/tests/adapter
 cp -r $ROOT/cl_multiview_stereo_amd/csrc $T/cl_multiview_stereo_amd/
 cp $ROOT/cl_multiview_stereo_amd/host/* $T/cl_multiview_stereo_amd/host/
 cp $ROOT/include/* $T/include/
-for f in "$@"; do cp "${f#*=}" $T/cl_multiview_stereo_amd/csrc/"${f%%=*}"; done
+for f in "$@"; do  # NAME=PATH: csrc/NAME, or include/NAME for an include/ header
+  n="${f%%=*}"
+  case $n in include/*) cp "${f#*=}" $T/"$n" ;; *) cp "${f#*=}" $T/cl_multiview_stereo_amd/csrc/"$n" ;; esac
+done
 make -s -j8 -C $T/cl_multiview_stereo_amd/csrc ../libmvs.so 2>&1 | grep -v dot6 || true
 mkdir -p $ROOT/ab
 cp $T/cl_multiview_stereo_amd/libmvs.so $ROOT/ab/libmvs_$TAG.so

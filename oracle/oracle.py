@@ -1,7 +1,9 @@
 """ORACLE TEST INFRASTRUCTURE -- ctypes front-end of oracle/_build/liboracle.so.
 
-CPU restatement of the reference hot path (oracle/mvs_oracle.c; PARITY
-UNPINNED -- see that file's header).  Only tests/, __graft_entry__.smoke() and
+CPU restatement of the reference hot path (oracle/mvs_oracle.c, pinned by the
+reference's kept outputs -- see that file's header and DESIGN.md 0).  MVS_ORACLE_LIB
+selects another build of the same source (the ASan build: scripts/oracle_asan.sh).
+Only tests/, __graft_entry__.smoke() and
 bench.py's cpu_baseline leg use it, and only as the checker / CPU baseline.
 Every function takes and returns numpy arrays in the reference layouts.
 """
@@ -14,7 +16,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+LIB_PATH = os.environ.get("MVS_ORACLE_LIB") or os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
 f32p = C.POINTER(C.c_float)

@@ -300,7 +300,11 @@ __device__ __forceinline__ int dot4(unsigned a, unsigned b, int c) {
 // smallest cost outside best+-1 is, per wave, its second smallest if its best
 // level is in that window, else its smallest -- exactly what k_wta's top-4
 // yields (ties resolved to the lower level by the strict < in level order).
-template <int K, int TH, int DPW, int NW, int BW, int PAR, bool FUSE>
+// NB: band buffers.  2: step t+1's bands land while step t computes.  1: one
+// buffer, staged at the start of each step behind a barrier (the other
+// resident workgroup computes meanwhile) -- the form that lets 32-level chunks
+// with tall vertical / diagonal bands keep two workgroups per CU (C4's 5-NN lists)
+template <int K, int TH, int DPW, int NW, int BW, int PAR, bool FUSE, int NB = 2>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_volume(const uint2* __restrict__ stats, const uint2* __restrict__ pk,
                                                     const NccRec* __restrict__ plan, NccArgs a,
                                                     float* __restrict__ vol, WtaOut wo) {
@@ -314,7 +318,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   constexpr unsigned HI_MASK = (K - 4) >= 4 ? 0xffffffffu : ((1u << (8 * (K - 4))) - 1u);
   extern __shared__ __align__(16) uint8_t smem[];
   const int nbuf = (a.pk_pairs + a.st_pairs) * BW;  // uint4 per neighbour buffer
-  u32x4* nbase = (u32x4*)smem;                      // 2 x {npk[pk_pairs][BW], nst[st_pairs][BW]}
+  u32x4* nbase = (u32x4*)smem;                      // NB x {npk[pk_pairs][BW], nst[st_pairs][BW]}
 
   // wave id made provably uniform: plan loads become scalar (SMEM), so no
   // vector-memory wait drains the in-flight LDS-DMA prefetch
@@ -377,7 +381,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // the band buffers and the merge area), read back at each chunk's fold --
   // 8 fewer long-lived VGPRs, so the loop needs no scratch reload (a VMEM
   // load there waits behind the in-flight band LDS-DMA)
-  float* srl = (float*)(smem + 16 * (size_t)max(2 * nbuf, FUSE ? 3 * NW * TH * 64 / 4 : 0));
+  float* srl = (float*)(smem + 16 * (size_t)max(NB * nbuf, FUSE ? 3 * NW * TH * 64 / 4 : 0));
   float wv0[TH], wv1[TH];  // FUSE: this wave's smallest and second smallest cost per row
   int wi0[TH];             //       level of the smallest
   // fused K = 7: the levels of rows 2m, 2m+1 as the halves of one register
@@ -385,7 +389,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // 128-VGPR cap (r03: 96 B of scratch, three of them spilled and reloaded at
   // every chunk's fold -- C5's fused launch moved 40 GB of scratch writes
   // against 0.5 GB of output); a half-select costs one v_bfi_b32 more per cell
-  constexpr bool PKI = FUSE && K == 7;
+  constexpr bool PKI = FUSE && (K == 7 || (PAR == kParMixed && DPW == 4));  // (K = 5: the mixed-parity 4-level kernels, C4)
   unsigned wi0p[TH / 2];
   if (FUSE) {
 #pragma unroll
@@ -547,7 +551,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   auto step = [&](int t, int n, int cprev, auto first) {
     constexpr bool FIRST = decltype(first)::value;
     const int n1 = n + 1 == nn ? 0 : n + 1;
-    if (t + 1 < T) stage(t + 1, n1, (t + 1) & 1);  // prefetch step t+1 while computing t
+    if (NB == 2 && t + 1 < T) stage(t + 1, n1, (t + 1) & 1);  // prefetch step t+1 while computing t
+    if (NB == 1 && t > 0) {  // this step's bands into the one buffer (step 0's: before the loop)
+      stage(t, n, 0);
+      __syncthreads();  // vmcnt(0): landed, for every wave
+    }
     // the previous chunk's costs are written here (its E, before this step
     // overwrites it), after this step's prefetch is issued and a whole step
     // before the barrier's vmcnt(0) (which also waits for stores): the write
@@ -556,7 +564,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
       store(cprev);
       if (!PEEL) reset();
     }
-    const u32x4* npk = nbase + (t & 1) * nbuf;
+    const u32x4* npk = nbase + (NB == 2 ? (t & 1) * nbuf : 0);
     const u32x4* nst = npk + a.pk_pairs * BW;
     const int ln = lane_now();
     int lvv[2 * DPW];  // one scalar load of this wave's level shifts for step t
@@ -729,7 +737,7 @@ NccPlan make_plan(const float* levels, int D, int nn, const float* fdx, const fl
   return p;
 }
 
-template <int K, int TH, int DPW, int NW, int BW, int PAR>
+template <int K, int TH, int DPW, int NW, int BW, int PAR, int NB = 2>
 int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
                   const WtaOut& wo, size_t lds) {
   hipStream_t s = ctx->stream;
@@ -741,7 +749,7 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
   a.tiles_per_xcd = (a.nref * a.ntiles + 7) / 8;
   a.nch = (a.D + DC - 1) / DC;
   dim3 g(8 * a.tiles_per_xcd);
-  auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, PAR, false> : k_ncc_volume<K, TH, DPW, NW, BW, PAR, true>;
+  auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, PAR, false, NB> : k_ncc_volume<K, TH, DPW, NW, BW, PAR, true, NB>;
   if (!vol) lds = std::max(lds, (size_t)3 * 4 * NW * TH * 64) + 4 * TH * 64;  // WTA partials; + s_r [64][TH]
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -754,13 +762,13 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
 // One reference view's variant: its shift plan for (K, TH = 8, DPW, NW) and
 // the band pair-row stride, if its double-buffered bands fit `cap` bytes of LDS.
 struct NccChoice {
-  int dpw = 0, nw = 0, bwt = 0;
+  int dpw = 0, nw = 0, bwt = 0, nb = 2;  // nb: band buffers (k_ncc_volume's NB)
   size_t cap = 0;
   NccPlan plan;
 };
 template <int K, int DPW, int NW>
 bool try_plan(const mvs_ctx* ctx, const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl,
-              size_t cap, NccChoice& o) {
+              size_t cap, NccChoice& o, int nb = 2) {
   NccPlan p = make_plan<K, 8, DPW, NW>(levels, D, nn, fdx, fdy, bl);
   // the band's pair-row stride is the template BW: the smallest of 64 / 80 /
   // 96 / 128 / 192 / 256 holding band_w, or a wider one forced through
@@ -768,8 +776,9 @@ bool try_plan(const mvs_ctx* ctx, const float* levels, int D, int nn, const floa
   // horizontal neighbour 64 + the chunk's shift range (C4: 71 / 79 / 95)
   const int bw = std::max(p.band_w, ctx->ncc_bw);
   const int bwt = bw <= 64 ? 64 : bw <= 80 ? 80 : bw <= 96 ? 96 : bw <= 128 ? 128 : bw <= 192 ? 192 : 256;
-  const size_t lds = 2 * 16 * (size_t)(p.pk_pairs + p.st_pairs) * bwt;
+  const size_t lds = nb * 16 * (size_t)(p.pk_pairs + p.st_pairs) * bwt;
   if (lds > cap || bw > 256) return false;
+  o.nb = nb;
   o.dpw = DPW;
   o.nw = NW;
   o.bwt = bwt;
@@ -812,8 +821,17 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
       MVS_NCC_TRY(1, 4)
     }
   }
+  // A K = 5 list whose double-buffered 32-level bands miss two workgroups per
+  // CU (C4's 5-NN lists: vertical and diagonal bands) tries them single-
+  // buffered before halving the chunk (k_ncc_volume's NB): C4 step 48.2 ->
+  // 47.6 ms (interleaved A/B, profiles/r04/abenv_c4_nb1.txt).  MVS_NCC_NB=2
+  // (read per call) keeps the double-buffered 16-level form.
+  const char* nbe = getenv("MVS_NCC_NB");
+  const bool nb1 = K == 5 && !(nbe && atoi(nbe) == 2);
   for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
     if (nw_pref >= 8 && dpw_pref >= 4) MVS_NCC_TRY(4, 8)
+    if (nb1 && cap <= 80 * 1024 && nw_pref >= 8 && dpw_pref >= 4 && !ok)
+      ok = try_plan<K, 4, 8>(ctx, levels, D, nn, fdx, fdy, bl, cap, o, 1);
     if (nw_pref >= 8 && dpw_pref >= 2) MVS_NCC_TRY(2, 8)
     if (dpw_pref >= 4) MVS_NCC_TRY(4, 4)
     if (dpw_pref >= 2) MVS_NCC_TRY(2, 4)
@@ -823,33 +841,35 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
   return ok;
 }
 
-template <int K, int DPW, int NW, int PAR>
+template <int K, int DPW, int NW, int PAR, int NB = 2>
 int launch_bw(mvs_ctx* ctx, int bwt, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
               const WtaOut& wo, size_t lds) {
-  if (bwt == 64) return launch_ncc_bw<K, 8, DPW, NW, 64, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 80) return launch_ncc_bw<K, 8, DPW, NW, 80, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 96) return launch_ncc_bw<K, 8, DPW, NW, 96, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
-  if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
-  return launch_ncc_bw<K, 8, DPW, NW, 256, PAR>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 64) return launch_ncc_bw<K, 8, DPW, NW, 64, PAR, NB>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 80) return launch_ncc_bw<K, 8, DPW, NW, 80, PAR, NB>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 96) return launch_ncc_bw<K, 8, DPW, NW, 96, PAR, NB>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 128) return launch_ncc_bw<K, 8, DPW, NW, 128, PAR, NB>(ctx, stats, pk, plan, a, vol, wo, lds);
+  if (bwt == 192) return launch_ncc_bw<K, 8, DPW, NW, 192, PAR, NB>(ctx, stats, pk, plan, a, vol, wo, lds);
+  return launch_ncc_bw<K, 8, DPW, NW, 256, PAR, NB>(ctx, stats, pk, plan, a, vol, wo, lds);
 }
 // the parity-specific kernels only where they occur: kParEven for K = 5
 // (horizontal bands, R = 2), kParOdd for K = 7 (R = 3)
 template <int K, int DPW, int NW>
 int launch_bw_par(mvs_ctx* ctx, int bwt, int par, const uint2* stats, const uint2* pk, const NccRec* plan,
-                  NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
+                  NccArgs& a, float* vol, const WtaOut& wo, size_t lds, int nb) {
   constexpr int KPAR = K == 5 ? kParEven : kParOdd;
+  if constexpr (K == 5 && DPW == 4 && NW == 8)  // single-buffered bands: C4's tall 5-NN bands (any parity)
+    if (nb == 1) return launch_bw<K, DPW, NW, kParMixed, 1>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);
   if (par == KPAR && !ctx->ncc_general) return launch_bw<K, DPW, NW, KPAR>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);
   return launch_bw<K, DPW, NW, kParMixed>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);
 }
 template <int K>
 int launch_variant(mvs_ctx* ctx, const NccChoice& c, int bwt, int par, const uint2* stats, const uint2* pk,
                    const NccRec* plan, NccArgs& a, float* vol, const WtaOut& wo, size_t lds) {
-  if (c.dpw == 4 && c.nw == 8) return launch_bw_par<K, 4, 8>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
-  if (c.dpw == 2 && c.nw == 8) return launch_bw_par<K, 2, 8>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
-  if (c.dpw == 4) return launch_bw_par<K, 4, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
-  if (c.dpw == 2) return launch_bw_par<K, 2, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
-  return launch_bw_par<K, 1, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds);
+  if (c.dpw == 4 && c.nw == 8) return launch_bw_par<K, 4, 8>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds, c.nb);
+  if (c.dpw == 2 && c.nw == 8) return launch_bw_par<K, 2, 8>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds, c.nb);
+  if (c.dpw == 4) return launch_bw_par<K, 4, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds, c.nb);
+  if (c.dpw == 2) return launch_bw_par<K, 2, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds, c.nb);
+  return launch_bw_par<K, 1, 4>(ctx, bwt, par, stats, pk, plan, a, vol, wo, lds, c.nb);
 }
 
 }  // namespace
@@ -915,11 +935,11 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
     int par = ch[i].plan.par();
     size_t cap = ch[i].cap;
     int j = i + 1;
-    while (!vol && j < n && j - i < maxrun && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw) {
+    while (!vol && j < n && j - i < maxrun && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw && ch[j].nb == ch[i].nb) {
       const int b2 = std::max(bwt, ch[j].bwt);
       const int p2 = std::max(pkp, ch[j].plan.pk_pairs), s2 = std::max(stp, ch[j].plan.st_pairs);
       const size_t c2 = std::min(cap, ch[j].cap);
-      if (2 * 16 * (size_t)(p2 + s2) * b2 > c2) break;
+      if (ch[i].nb * 16 * (size_t)(p2 + s2) * b2 > c2) break;
       bwt = b2;
       pkp = p2;
       stp = s2;
@@ -947,7 +967,7 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
     const int32_t* dev = plan_upload(ctx, table, &rc);
     if (rc) return rc;
     const WtaOut wo{levels_dev, disp ? disp + P * i : nullptr, conf ? conf + P * i : nullptr};
-    const size_t lds = 2 * 16 * (size_t)(pkp + stp) * bwt;
+    const size_t lds = ch[i].nb * 16 * (size_t)(pkp + stp) * bwt;
     rc = K == 5 ? launch_variant<5>(ctx, ch[i], bwt, par, stats, pk, (const NccRec*)dev, a, vol, wo, lds)
                 : launch_variant<7>(ctx, ch[i], bwt, par, stats, pk, (const NccRec*)dev, a, vol, wo, lds);
     if (rc) return rc;

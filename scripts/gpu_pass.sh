@@ -9,6 +9,7 @@
 #   bench            the driver's command (bench.py --gpus 1 --steps 20 --warmup 5) -> bench.json
 #   bench:CFG        bench.py --config CFG --no-cpu-baseline  -> bench_CFG.json
 #   ab:CFG           interleaved A/B (ab/libmvs_A.so vs the in-tree build), 2 rounds -> ab_CFG.txt
+#   abenv:CFG:VAR=V  interleaved A/B of one environment setting (A: unset, B: VAR=V), 2 rounds
 #   trace:CFG        rocprofv3 --kernel-trace --stats of bench.py --config CFG --steps 5
 #   pmc:CFG          scripts/profile.sh's PMC passes for CFG (profiles/pmc_*_CFG.json)
 set -u
@@ -48,6 +49,18 @@ for s in "$@"; do
         done
       done
       unset MVS_LIB ;;
+    abenv:*)
+      X=${s#abenv:}; C=${X%%:*}; KV=${X#*:}; VAR=${KV%%=*}
+      for r in 1 2; do
+        for side in A B; do
+          if [ $side = A ]; then unset $VAR; else export "$KV"; fi
+          timeout -k 10 300 python3 bench.py --config $C --no-cpu-baseline --no-sharded --no-reference-cost \
+            --no-reference-defaults ${ABARGS:-} > $O/abenv_$side.json 2> $O/abenv_$side.err || fail "$s $side" $O/abenv_$side.err
+          python3 -c "import json;j=json.load(open('$O/abenv_$side.json'));print('$C $KV $side', j['ms_per_step'], j['value'], (j.get('roofline_sweep') or {}).get('avg_ms_per_view'))" \
+            | tee -a $O/abenv_$C.txt
+        done
+      done
+      unset $VAR ;;
     trace:*)
       C=${s#trace:}
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_$C -o run -- python3 bench.py --config $C \

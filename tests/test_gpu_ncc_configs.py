@@ -114,12 +114,15 @@ def test_c5_full_size_bands(eng):
         same(fd[y0:y1], od[rows], f"fused disp rows {y0}..{y1}")
 
 
-@pytest.mark.parametrize("bl", [1.0, 1.0359])
-def test_c4_geometry(eng, bl):
+@pytest.mark.parametrize("bl,nb", [(1.0, "1"), (1.0359, "1"), (1.0, "2"), (1.0359, "2")])
+def test_c4_geometry(eng, bl, nb, monkeypatch):
     """C4's array (8x4, 5 nearest neighbours: horizontal, vertical and
     diagonal) at 128 levels on a cropped image.  The taller bands of the
     vertical neighbours must select the 2- and 1-level-per-wave variants the
-    full-size C4 run uses, and all of them must match the oracle."""
+    full-size C4 run uses, and all of them must match the oracle.  nb = "1"
+    (the default, MVS_NCC_NB): 32-level chunks with single-buffered bands where the
+    double-buffered ones miss two workgroups per CU; "2": the 16-level form."""
+    monkeypatch.setenv("MVS_NCC_NB", nb)
     aw, ah, W, H = 8, 4, 256, 72
     stack, _ = synth.make_stack(W, H, aw, ah, 0, 127, bl, 0x5EED + 4)
     cam = _array(aw, ah, 0, 127, knn=5, bl=bl)
@@ -141,7 +144,10 @@ def test_c4_geometry(eng, bl):
         same(fd, od, f"fused disp z{z}")
         same(fc, oc, f"fused conf z{z}")
     dpws = {v[0] for v in variants}
-    assert dpws & {1, 2}, f"C4 geometry should need a narrower variant, saw {sorted(variants)}"
+    if nb == "1":  # every list but the corner views' (a neighbour two rows away) takes 32-level chunks
+        assert 4 in dpws, f"single-buffered 32-level chunks expected, saw {sorted(variants)}"
+    else:
+        assert dpws & {1, 2}, f"C4 geometry should need a narrower variant, saw {sorted(variants)}"
 
 
 _VARIANTS = [(8, 4), (8, 2), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation

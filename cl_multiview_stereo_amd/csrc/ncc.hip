@@ -823,9 +823,12 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
   }
   // A K = 5 list whose double-buffered 32-level bands miss two workgroups per
   // CU (C4's 5-NN lists: vertical and diagonal bands) tries them single-
-  // buffered before halving the chunk (k_ncc_volume's NB): C4 step 48.2 ->
-  // 47.6 ms (interleaved A/B, profiles/r04/abenv_c4_nb1.txt).  MVS_NCC_NB=2
-  // (read per call) keeps the double-buffered 16-level form.
+  // buffered before halving the chunk (k_ncc_volume's NB), and a list too
+  // tall even for that (C4's corner views: a neighbour two rows away) takes
+  // 8 waves x 2 levels single-buffered before 4 waves: C4 step 48.1 -> 46.6 ms,
+  // fused sweep 0.71 -> 0.66 ms per view (interleaved A/B,
+  // profiles/r04/abenv_c4_nb1_corner.txt).  MVS_NCC_NB=2 (read per call)
+  // keeps the double-buffered forms.
   const char* nbe = getenv("MVS_NCC_NB");
   const bool nb1 = K == 5 && !(nbe && atoi(nbe) == 2);
   for (size_t cap : {(size_t)80 * 1024, (size_t)160 * 1024}) {
@@ -833,6 +836,8 @@ bool choose_variant(const mvs_ctx* ctx, const float* levels, int D, int nn, cons
     if (nb1 && cap <= 80 * 1024 && nw_pref >= 8 && dpw_pref >= 4 && !ok)
       ok = try_plan<K, 4, 8>(ctx, levels, D, nn, fdx, fdy, bl, cap, o, 1);
     if (nw_pref >= 8 && dpw_pref >= 2) MVS_NCC_TRY(2, 8)
+    if (nb1 && cap <= 80 * 1024 && nw_pref >= 8 && dpw_pref >= 2 && !ok)  // (C4's corner views)
+      ok = try_plan<K, 2, 8>(ctx, levels, D, nn, fdx, fdy, bl, cap, o, 1);
     if (dpw_pref >= 4) MVS_NCC_TRY(4, 4)
     if (dpw_pref >= 2) MVS_NCC_TRY(2, 4)
     MVS_NCC_TRY(1, 4)
@@ -857,7 +862,7 @@ template <int K, int DPW, int NW>
 int launch_bw_par(mvs_ctx* ctx, int bwt, int par, const uint2* stats, const uint2* pk, const NccRec* plan,
                   NccArgs& a, float* vol, const WtaOut& wo, size_t lds, int nb) {
   constexpr int KPAR = K == 5 ? kParEven : kParOdd;
-  if constexpr (K == 5 && DPW == 4 && NW == 8)  // single-buffered bands: C4's tall 5-NN bands (any parity)
+  if constexpr (K == 5 && DPW >= 2 && NW == 8)  // single-buffered bands: C4's tall 5-NN bands (any parity)
     if (nb == 1) return launch_bw<K, DPW, NW, kParMixed, 1>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);
   if (par == KPAR && !ctx->ncc_general) return launch_bw<K, DPW, NW, KPAR>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);
   return launch_bw<K, DPW, NW, kParMixed>(ctx, bwt, stats, pk, plan, a, vol, wo, lds);

@@ -264,12 +264,16 @@ __device__ __forceinline__ void read_stat_pairs(const u32x4* col, int r0, f32x4 
 #pragma unroll
     for (int i = 0; i < N / 2; i++) v[i] = __builtin_bit_cast(f32x4, p[i * BW]);
   } else {
-    f32x4 prev = __builtin_bit_cast(f32x4, p[0]);
+    // only the 16 needed dwords, as ds_read2_b32 pairs ({a, b} of one stored
+    // row): no stored pair held whole, so the odd path needs no more registers
+    // than the even one (the whole-pair form kept N/2 + 1 pairs live, and the
+    // fused mixed-parity kernels spilled their fold accumulators for it)
+    const float* f = (const float*)p;
 #pragma unroll
     for (int i = 0; i < N / 2; i++) {
-      const f32x4 nx = __builtin_bit_cast(f32x4, p[(i + 1) * BW]);
-      v[i] = f32x4{prev.y, nx.x, prev.w, nx.z};
-      prev = nx;
+      const float* q0 = f + i * BW * 4;        // stored pair i: second rows (y, w)
+      const float* q1 = f + (i + 1) * BW * 4;  // stored pair i + 1: first rows (x, z)
+      v[i] = f32x4{q0[1], q1[0], q0[3], q1[2]};
     }
   }
 }

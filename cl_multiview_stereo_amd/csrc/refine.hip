@@ -817,6 +817,9 @@ __global__ void k_spixl_to_image(const float* __restrict__ spixl, const LT* __re
   disp[P * z + (long)W * y + x] = v / t[5];
 }
 
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+
 // The same map, 4 consecutive pixels per thread (W % 4 == 0): one 16-B (u32
 // labels) or 8-B (u16) label load and one 16-B store per thread, the record gathers as buffer loads
 // with 32-bit offsets inside view z's records (a label is the superpixel
@@ -840,16 +843,21 @@ __global__ __launch_bounds__(256) void k_spixl_to_image4(const float* __restrict
     const uint2 id4 = *(const uint2*)(labels + p);
     ids[0] = id4.x & 0xffffu, ids[1] = id4.x >> 16, ids[2] = id4.y & 0xffffu, ids[3] = id4.y >> 16;
   }
+  // three gathers per pixel, (x, y) of the centre, d, and the normal: the
+  // kernel is bound by the gather instructions' address processing, not by
+  // their bytes (six dword gathers per pixel: 0.17 ms at C4)
   float s1[4], s2[4], t0[4], t3[4], t4[4], t5[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int os = (int)ids[k] * 32, ot = (int)ids[k] * 24;
-    s1[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsp, os + 4, 0, 0));
-    s2[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsp, os + 8, 0, 0));
+    const u32x2 sxy = __builtin_amdgcn_raw_buffer_load_b64(rsp, os + 4, 0, 0);
+    const u32x3 tn = __builtin_amdgcn_raw_buffer_load_b96(rst, ot + 12, 0, 0);
+    s1[k] = __uint_as_float(sxy.x);
+    s2[k] = __uint_as_float(sxy.y);
     t0[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot, 0, 0));
-    t3[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot + 12, 0, 0));
-    t4[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot + 16, 0, 0));
-    t5[k] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rst, ot + 20, 0, 0));
+    t3[k] = __uint_as_float(tn.x);
+    t4[k] = __uint_as_float(tn.y);
+    t5[k] = __uint_as_float(tn.z);
   }
   float o[4];
 #pragma unroll

@@ -345,6 +345,48 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v0, uint32_t v1, uint3
   return s;
 }
 
+// wave_tree for several channels at once, from their in-lane sums sX =
+// (v0 + v2) + (v1 + v3).  The two-register lane swaps pair the channels up
+// instead of swapping each with itself: v_permlane32_swap(A, B) leaves the
+// stride-32 sums of A in lanes 0-31 and of B in lanes 32-63, and
+// v_permlane16_swap of two such registers puts the stride-16 sums of A, C, B,
+// D in the four 16-lane rows, so one DPP row_shl chain finishes all four.
+// Every channel's additions are wave_tree's, in its order.  Result lanes:
+// A 0, C 16, B 32, D 48 (wave_tree2s: A 0, B 32).
+__device__ __forceinline__ float dpp_rows_sum(float s) {
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x108, 0xf, 0xf, true));
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x104, 0xf, 0xf, true));
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x102, 0xf, 0xf, true));
+  s = s + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x101, 0xf, 0xf, true));
+  return s;
+}
+__device__ __forceinline__ float halves_sum(float a, float b) {  // A in lanes 0-31, B in 32-63
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float wave_tree4s(float sA, float sB, float sC, float sD) {
+  const float X = halves_sum(sA, sB), Z = halves_sum(sC, sD);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(X), __float_as_uint(Z), false, false);
+  return dpp_rows_sum(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float wave_tree2s(float sA, float sB) {
+  const float X = halves_sum(sA, sB);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(X), __float_as_uint(X), false, false);
+  return dpp_rows_sum(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+}
+// two integer sums (any order gives the same value): A in lane 0, B in lane 32
+__device__ __forceinline__ uint32_t wave_sum2_u32(uint32_t sA, uint32_t sB) {
+  const auto p = __builtin_amdgcn_permlane32_swap(sA, sB, false, false);
+  uint32_t s = p[0] + p[1];
+  const auto r = __builtin_amdgcn_permlane16_swap(s, s, false, false);
+  s = r[0] + r[1];
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x108, 0xf, 0xf, true);
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x104, 0xf, 0xf, true);
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x102, 0xf, 0xf, true);
+  s = s + (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x101, 0xf, 0xf, true);
+  return s;
+}
+
 // One WAVE per superpixel (4 per workgroup): the wave walks the G window
 // tiles in order, each tile's 256 pixels as 4 per lane, tree-reduced in the
 // reference's order (wave_tree), and lane 0 sums the tile partials in tile
@@ -634,12 +676,240 @@ __global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__
   }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// The same wave per tile for the reference's active 2x2 loop when S = 32 or
+// 64 (C2-C4's S = 32).  The tile's candidate cells are then the same four for
+// all its pixels: dX = (col + S/2) / S - cxg cannot change inside a 16-column
+// tile when S/2 is a multiple of 16 (likewise dY), so
+//  * the pixel test is branch-free: a candidate is taken when d2 is below the
+//    best d2 by more than the sqrt rounding can hide, or, for the first one,
+//    below 9e11 (k_assign's fast tests); only a lane meeting a near tie (or a
+//    huge d2) re-runs k_assign's exact loop with its square roots;
+//  * the update reduces only the four candidate cells, their trees
+//    interleaved (16 independent chains per wave instead of one cell's four at
+//    a time behind a branch); the other in-image cells of the 3x3 around the
+//    tile, which no pixel of the tile can join, get the exact zeros k_update_tiles
+//    would write for them.
+// (The 9-cell loop measured 71-83 us per C2 launch: 40 % of its wave cycles
+// stalled on instruction dependencies, 632 SALU instructions per wave.)
+// S16 = S / 16 (2: S = 32, 4: S = 64): divisions by constants.  Grid
+// ((ntx + 3) / 4, nty, V): the tile is (4 blockIdx.x + wave, blockIdx.y).
+template <int S16>
+__global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict__ lab,
+                                                       const float* __restrict__ spixl, int W, int H, int mw,
+                                                       int mh, float xy_n, float col_n, float weight, int G, int cpl,
+                                                       int ntx, uint32_t* __restrict__ labels,
+                                                       float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int TX = blockIdx.x * 4 + wave, TY = blockIdx.y, z = blockIdx.z;
+  if (TX >= ntx) return;  // whole wave; no workgroup barriers below
+  constexpr int s16 = S16;
+  const int cxg = TX / S16, cyg = TY / S16;  // the tile's cell
+  // (16 TX + S/2) / S with S = 16 S16
+  const int dX = (TX + S16 / 2) / S16 - cxg, dY = (TY + S16 / 2) / S16 - cyg;
+  const long P = (long)W * H;
+  const float4* L = lab + (long)z * P;
+  const float* sp = spixl + 8L * z * mw * mh;
+  // candidate i = 2 ii + jj in k_assign's loop order (slic_cand<false>)
+  int ccx[4], ccy[4];
+  bool cok[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    int ox, oy;
+    slic_cand<false>(i >> 1, i & 1, dX, dY, ox, oy);
+    ccx[i] = cxg + ox;
+    ccy[i] = cyg + oy;
+    cok[i] = ccx[i] >= 0 && ccy[i] >= 0 && ccx[i] < mw && ccy[i] < mh;
+  }
+  // the candidates' centres, wave-uniform, as pairs (0, 1) and (2, 3) for the
+  // packed two-candidate distance below; a cell outside the map gets a NaN
+  // centre, so its d2 is NaN: never taken, never a near tie
+  f32x2 ccxp[2], ccyp[2], cLp[2], cap[2], cbp[2];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    float v[5];
+    const float* cc = sp + 8 * (cok[i] ? ccy[i] * mw + ccx[i] : 0);
+#pragma unroll
+    for (int f = 0; f < 5; f++) v[f] = cc[1 + f];  // (cell 0 stands in for an outside one)
+#pragma unroll
+    for (int f = 0; f < 5; f++) v[f] = cok[i] ? v[f] : __builtin_nanf("");
+    ccxp[i >> 1][i & 1] = v[0];
+    ccyp[i >> 1][i & 1] = v[1];
+    cLp[i >> 1][i & 1] = v[2];
+    cap[i >> 1][i & 1] = v[3];
+    cbp[i >> 1][i & 1] = v[4];
+  }
+  const int lx = lane & 15, ly0 = lane >> 4;  // local index k = lane + 64*m, as the reference tile
+  float4 c[4];
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int px = TX * 16 + lx, py = TY * 16 + ly0 + 4 * m;
+    const bool in = px < W && py < H;
+    c[m] = in ? L[(long)py * W + px] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float cid[4];  // the candidates' labels as k_assign forms them
+#pragma unroll
+  for (int i = 0; i < 4; i++) cid[i] = (float)(ccy[i] * mw + ccx[i]);
+  uint32_t lbl[4];
+  int win[4];  // the pixel's candidate (-1: none, or outside the image)
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int col = TX * 16 + lx, row = TY * 16 + ly0 + 4 * m;
+    // slic_dist2 for two candidates at once (packed FP32, the same operations
+    // in the same order)
+    float d2[4];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const f32x2 dl = f32x2{c[m].x, c[m].x} - cLp[h];
+      f32x2 ac = dl * dl;
+      const f32x2 da = f32x2{c[m].y, c[m].y} - cap[h];
+      ac = ac + da * da;
+      const f32x2 db = f32x2{c[m].z, c[m].z} - cbp[h];
+      ac = ac + db * db;
+      const f32x2 dx = f32x2{(float)col, (float)col} - ccxp[h];
+      f32x2 bc = dx * dx;
+      const f32x2 dy = f32x2{(float)row, (float)row} - ccyp[h];
+      bc = bc + dy * dy;
+      const f32x2 d = (ac * f32x2{col_n, col_n}) + f32x2{weight, weight} * (bc * f32x2{xy_n, xy_n});
+      d2[2 * h] = d.x;
+      d2[2 * h + 1] = d.y;
+    }
+    // k_assign's loop keeps the first candidate of least sqrtf(d2) (strict <),
+    // sqrtf being monotone: the first of least d2, unless a later-looking d2
+    // lies so close above the least that the square roots may round together
+    // (d2 * 0.99999905 <= least: k_assign's own near-tie test), or the least
+    // is not below the 9e11 the first take is sure of.  Such a lane re-runs
+    // k_assign's loop.  NaN (outside-map) candidates drop out of the min.
+    const float lo = fminf(fminf(d2[0], d2[1]), fminf(d2[2], d2[3]));
+    int w = d2[3] == lo ? 3 : -1;
+    w = d2[2] == lo ? 2 : w;
+    w = d2[1] == lo ? 1 : w;
+    w = d2[0] == lo ? 0 : w;
+    // (as float maxima, not short-circuit logic, which compiled to a branch
+    // per candidate: lo - x >= 0 iff x <= lo for finite x)
+    float am = lo < 9.0e11f ? -1.0f : 1.0f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) am = fmaxf(am, d2[i] > lo ? lo - d2[i] * 0.99999905f : -1.0f);
+    const bool amb = am >= 0.0f;
+    float min_id = w == 0 ? cid[0] : w == 1 ? cid[1] : w == 2 ? cid[2] : w == 3 ? cid[3] : -1.0f;
+    if (amb) {  // k_assign's loop, square roots and all
+      float best2 = 0.0f;
+      bool have = false;
+      min_id = -1.0f;
+      w = -1;
+      for (int i = 0; i < 4; i++) {
+        bool take;
+        if (!have) {
+          take = d2[i] < 9.0e11f || sqrtf(d2[i]) < 999999.9999f;
+        } else if (d2[i] >= best2) {
+          take = false;
+        } else if (d2[i] < best2 * 0.99999905f) {
+          take = true;
+        } else {
+          take = sqrtf(d2[i]) < sqrtf(best2);
+        }
+        take = take && cok[i];
+        best2 = take ? d2[i] : best2;
+        min_id = take ? cid[i] : min_id;
+        w = take ? i : w;
+        have = have || take;
+      }
+    }
+    const bool in = col < W && row < H;
+    lbl[m] = in ? (uint32_t)min_id : 0xffffffffu;
+    win[m] = in ? w : -1;
+    if (in) labels[(long)z * P + (long)row * W + col] = lbl[m];
+  }
+  if (!part) return;
+  float* out = part + (long)z * mw * mh * G * 6;
+  // the candidate cells some pixel of the tile joined (a wave-uniform mask)
+  unsigned pres = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const bool mi = win[0] == i || win[1] == i || win[2] == i || win[3] == i;
+    pres |= __ballot(mi) != 0 ? 1u << i : 0u;
+  }
+  pres = __builtin_amdgcn_readfirstlane(pres);
+  const unsigned joined_mask = pres;
+  // the present cells' tile partials, two cells' trees interleaved per pass
+  // (one pass for a tile inside one or two superpixels, the usual case)
+  while (pres) {
+    const int i0 = __builtin_ctz(pres);
+    pres &= pres - 1;
+    const int i1 = pres ? __builtin_ctz(pres) : i0;  // i1 == i0: a second copy, not stored
+    pres &= pres ? pres - 1 : 0u;
+    float sL[2], sa[2], sb[2];
+    uint32_t sq[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {  // the in-lane step of the trees
+      const int i = h == 0 ? i0 : i1;
+      bool mem[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) mem[m] = win[m] == i;
+      uint32_t pk[4];
+      float vL[4], va[4], vb[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        pk[m] = mem[m] ? (uint32_t)lx | (uint32_t)(ly0 + 4 * m) << 12 | 1u << 24 : 0u;
+        vL[m] = mem[m] ? c[m].x : 0.f;
+        va[m] = mem[m] ? c[m].y : 0.f;
+        vb[m] = mem[m] ? c[m].z : 0.f;
+      }
+      sq[h] = (pk[0] + pk[2]) + (pk[1] + pk[3]);
+      sL[h] = (vL[0] + vL[2]) + (vL[1] + vL[3]);
+      sa[h] = (va[0] + va[2]) + (va[1] + va[3]);
+      sb[h] = (vb[0] + vb[2]) + (vb[1] + vb[3]);
+    }
+    const float T1 = wave_tree4s(sL[0], sa[0], sb[0], sL[1]);  // lanes 0: L0, 32: a0, 16: b0, 48: L1
+    const float T2 = wave_tree2s(sa[1], sb[1]);                // lanes 0: a1, 32: b1
+    const uint32_t Q = wave_sum2_u32(sq[0], sq[1]);            // lane 32 h: cell h's x, y, count
+    const bool two = i1 != i0;
+    long base[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int i = h == 0 ? i0 : i1;
+      const int gx = i == 0 ? ccx[0] : i == 1 ? ccx[1] : i == 2 ? ccx[2] : ccx[3];
+      const int gy = i == 0 ? ccy[0] : i == 1 ? ccy[1] : i == 2 ? ccy[2] : ccy[3];
+      const int t = (TY - (gy - 1) * s16) * cpl + (TX - (gx - 1) * s16);
+      base[h] = ((long)(gy * mw + gx) * G + t) * 6;
+    }
+    // each result stored from the lane holding it
+    if (lane == 0 || (lane == 32 && two)) {
+      const int cnt = (Q >> 24) ? (int)(Q >> 24) : 256;  // present: at least one member
+      float* o = out + (lane == 0 ? base[0] : base[1]);
+      o[0] = (float)((int)(Q & 0xfffu) + cnt * 16 * TX);
+      o[1] = (float)((int)((Q >> 12) & 0xfffu) + cnt * 16 * TY);
+      o[5] = (float)cnt;
+    }
+    if (lane == 0 || lane == 16 || lane == 32 || (lane == 48 && two))
+      out[lane == 0 ? base[0] + 2 : lane == 16 ? base[0] + 4 : lane == 32 ? base[0] + 3 : base[1] + 2] = T1;
+    if (two && (lane == 0 || lane == 32)) out[lane == 0 ? base[1] + 3 : base[1] + 4] = T2;
+  }
+  // exact zeros for every other in-image cell of the 3x3 around the tile (no
+  // pixel of the tile joined it): lane 6 j + ch, cell j
+  if (lane < 54) {
+    const int j = lane / 6, ch = lane - 6 * j;
+    const int gx = cxg - 1 + j % 3, gy = cyg - 1 + j / 3;
+    bool joined = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) joined = joined || (((joined_mask >> i) & 1u) && gx == ccx[i] && gy == ccy[i]);
+    if (!joined && gx >= 0 && gy >= 0 && gx < mw && gy < mh) {
+      const int t = (TY - (gy - 1) * s16) * cpl + (TX - (gx - 1) * s16);
+      out[((long)(gy * mw + gx) * G + t) * 6 + ch] = 0.0f;
+    }
+  }
+}
+
 // 8 lanes per superpixel, lane c < 6 summing channel c of the G partials in
 // tile order (the reference's order; a tile outside the image adds an exact
 // +0, which leaves the running sum unchanged: it starts at +0 and a sum is
 // -0 only when both terms are).  All G loads are independent of the sums,
 // so they are issued ahead -- one thread walking all six channels was
 // load-latency-bound (14 us per launch at C2).
+// CPL > 0: cpl = CPL (G = CPL^2; S = 32: 6), every partial's load issued
+// before the sum (9.2 us per C2 launch with four in flight)
+template <int CPL>
 __global__ __launch_bounds__(256) void k_update_finalize(const float* __restrict__ part, int mw, int mh, int S,
                                                          int G, int cpl, int ntx, int nty,
                                                          float* __restrict__ spixl) {
@@ -649,14 +919,27 @@ __global__ __launch_bounds__(256) void k_update_finalize(const float* __restrict
   const int gx = spc % mw, gy = spc / mw, s16 = S / 16;
   const float* pp = part + ((long)z * mw * mh + spc) * G * 6 + (c < 6 ? c : 5);
   float acc = 0.f;
-  int tx = 0, ty = 0;
+  if (CPL > 0) {
+    constexpr int GT = CPL > 0 ? CPL * CPL : 1;
+    float v[GT];
+#pragma unroll
+    for (int t = 0; t < GT; t++) v[t] = pp[t * 6];
+#pragma unroll
+    for (int t = 0; t < GT; t++) {
+      const int TX = (gx - 1) * s16 + t % CPL, TY = (gy - 1) * s16 + t / CPL;
+      const bool in = TX >= 0 && TY >= 0 && TX < ntx && TY < nty;  // outside the image: the reference adds 0
+      acc = acc + (in ? v[t] : 0.f);
+    }
+  } else {
+    int tx = 0, ty = 0;
 #pragma unroll 4
-  for (int t = 0; t < G; t++) {
-    const int TX = (gx - 1) * s16 + tx, TY = (gy - 1) * s16 + ty;
-    const bool in = TX >= 0 && TY >= 0 && TX < ntx && TY < nty;  // outside the image: the reference adds 0
-    const float v = pp[t * 6];
-    acc = acc + (in ? v : 0.f);
-    if (++tx == cpl) { tx = 0; ty++; }
+    for (int t = 0; t < G; t++) {
+      const int TX = (gx - 1) * s16 + tx, TY = (gy - 1) * s16 + ty;
+      const bool in = TX >= 0 && TY >= 0 && TX < ntx && TY < nty;  // outside the image: the reference adds 0
+      const float v = pp[t * 6];
+      acc = acc + (in ? v : 0.f);
+      if (++tx == cpl) { tx = 0; ty++; }
+    }
   }
   const float n = __shfl(acc, (threadIdx.x & 63 & ~7) + 5);
   if (!live || c > 6) return;
@@ -757,8 +1040,14 @@ int launch_assign_tiles(hipStream_t s, const float* lab, const float* spixl, int
   int mw = map_dim(W, S), mh = map_dim(H, S);
   int G = (3 * S / kLocal) * (3 * S / kLocal), cpl = S * 3 / kLocal;
   int ntx = (W + 15) / 16, nty = (H + 15) / 16;
-  hipLaunchKernelGGL(search ? k_assign_tiles<true> : k_assign_tiles<false>, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, spixl, W,
-                     H, S, mw, mh, xy_n, col_n, weight, G, cpl, ntx, nty, labels, part);
+  // MVS_SLIC_TILES9=1 (read per call): the 9-cell kernel for S % 32 == 0 too (A/B)
+  const char* t9 = getenv("MVS_SLIC_TILES9");
+  if (!search && (S == 32 || S == 64) && !(t9 && atoi(t9) == 1))
+    hipLaunchKernelGGL(S == 32 ? k_assign_tiles4<2> : k_assign_tiles4<4>, dim3((ntx + 3) / 4, nty, V), dim3(256), 0,
+                       s, (const float4*)lab, spixl, W, H, mw, mh, xy_n, col_n, weight, G, cpl, ntx, labels, part);
+  else
+    hipLaunchKernelGGL(search ? k_assign_tiles<true> : k_assign_tiles<false>, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, spixl, W,
+                       H, S, mw, mh, xy_n, col_n, weight, G, cpl, ntx, nty, labels, part);
   MVS_LAUNCH_CHECK("k_assign_tiles");
   return 0;
 }
@@ -767,8 +1056,8 @@ int launch_update_finalize(hipStream_t s, const float* part, int V, int W, int H
   int mw = map_dim(W, S), mh = map_dim(H, S);
   int G = (3 * S / kLocal) * (3 * S / kLocal), cpl = S * 3 / kLocal;
   int ntx = (W + 15) / 16, nty = (H + 15) / 16;
-  hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 31) / 32, V), dim3(256), 0, s, part, mw, mh, S, G, cpl, ntx,
-                     nty, spixl);
+  hipLaunchKernelGGL(cpl == 6 ? k_update_finalize<6> : k_update_finalize<0>, dim3((mw * mh + 31) / 32, V), dim3(256),
+                     0, s, part, mw, mh, S, G, cpl, ntx, nty, spixl);
   MVS_LAUNCH_CHECK("k_update_finalize");
   return 0;
 }
@@ -791,8 +1080,8 @@ int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V
     hipLaunchKernelGGL(k_update_tiles, dim3((ntx * nty + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, labels,
                        W, H, S, mw, mh, G, cpl, ntx, nty, part);
     MVS_LAUNCH_CHECK("k_update_tiles");
-    hipLaunchKernelGGL(k_update_finalize, dim3((mw * mh + 31) / 32, V), dim3(256), 0, s, part, mw, mh, S, G, cpl,
-                       ntx, nty, spixl);
+    hipLaunchKernelGGL(cpl == 6 ? k_update_finalize<6> : k_update_finalize<0>, dim3((mw * mh + 31) / 32, V),
+                       dim3(256), 0, s, part, mw, mh, S, G, cpl, ntx, nty, spixl);
     MVS_LAUNCH_CHECK("k_update_finalize");
     return 0;
   }

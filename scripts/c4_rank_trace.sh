@@ -17,4 +17,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
   --load-rec /tmp/c4rec.pt --only-rank ${RANK:-7} --steps 5 > $O/rank.json 2> $O/rank.err || { tail -5 $O/rank.err; exit 1; }
 cat $O/rank.json
 f=$(find $O/trace -name "*kernel_stats.csv" | head -1); cut -d, -f1-5 "$f" | head -30
+t=$(find $O/trace -name "*kernel_trace.csv" | head -1); python3 scripts/trace_summary.py "$t" ${STEPS_IN_TRACE:-6} > $O/summary.txt; cat $O/summary.txt
 rm -f /tmp/c4rec.pt

@@ -109,6 +109,7 @@ struct SweepArgs {
 // TL = false (no re-laid views in this call, e.g. a horizontal array): the
 // row-major addressing folds to yp W + xp at compile time -- the general
 // form's extra multiply-add per tap cost C2 (5x1 array) 173 -> 224 us.
+typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
 template <int LPS, bool TL>
 __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ lab, float* __restrict__ spixl,
                                                      const uint8_t* __restrict__ rep,
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
                                                      const float4* __restrict__ labT,
                                                      const int* __restrict__ tslot, long tstride) {
   __shared__ float4 refc[8][25];
-  __shared__ int2 refxy[8][25];
+  __shared__ float2 refxy[8][25];  // (float)xr, (float)yr; xr = -1e9 for a tap outside the image
   __shared__ float wbest[4];
   __shared__ int wbi[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -147,8 +148,9 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
     int i = ll / 5 - 2, j = ll % 5 - 2;  // tap order: i (x) outer, j (y) inner
     int xr = (int)(cx + (float)i * stx);
     int yr = (int)(cy + (float)j * sty);
-    refxy[slot][ll] = make_int2(xr, yr);
     bool in = xr >= 0 && yr >= 0 && xr < a.W && yr < a.H;
+    // (float)xr is exact; an outside reference tap projects outside too
+    refxy[slot][ll] = make_float2(in ? (float)xr : -1.0e9f, (float)yr);
     refc[slot][ll] = in ? labz[(long)yr * a.W + xr] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
@@ -168,6 +170,9 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       const int kind = !TL ? 0 : ddx == 0 ? 1 : ddx == ddy ? 2 : ddx == -ddy ? 3 : 0;
       const int ts = TL && kind ? tslot[4 * view + kind] : -1;
       const float4* labv = TL && ts >= 0 ? labT + (long)ts * tstride : lab + (long)view * P;
+      // 32-bit byte offsets into the view's layout (the launcher checks the
+      // size): one address add per tap instead of 64-bit index arithmetic
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)labv, 0, 0x7fffffff, 0x00020000);
       // element index = off + x sxs + y sys in the view's layout
       const int sxs = !TL || ts < 0 ? 1 : a.H;
       const int sys = !TL || ts < 0 ? a.W : kind == 1 ? 1 : kind == 2 ? 1 - a.H : a.H + 1;
@@ -178,11 +183,13 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       // independent and in flight together instead of one per branch
 #pragma unroll 5
       for (int t = 0; t < 25; t++) {
-        int2 r = refxy[slot][t];
-        int xp = (int)((float)r.x - fdx);
-        int yp = (int)((float)r.y - fdy);
-        const bool in = r.x >= 0 && r.y >= 0 && xp >= 0 && yp >= 0 && r.x < a.W && r.y < a.H && xp < a.W && yp < a.H;
-        const float4 B = labv[in ? off + yp * sys + xp * sxs : 0];
+        const float2 r = refxy[slot][t];
+        const int xp = (int)(r.x - fdx);
+        const int yp = (int)(r.y - fdy);
+        const bool in = (unsigned)xp < (unsigned)a.W && (unsigned)yp < (unsigned)a.H;
+        const int bo = in ? (off + yp * sys + xp * sxs) * 16 : 0;  // an outside tap reads pixel 0, dropped below
+        const u32x3 bv = __builtin_amdgcn_raw_buffer_load_b96(rs, bo, 0, 0);
+        const float3 B = make_float3(__uint_as_float(bv.x), __uint_as_float(bv.y), __uint_as_float(bv.z));
         const float4 A = refc[slot][t];
         float ad = fabsf(A.x - B.x) + fabsf(A.y - B.y);
         ad = ad + fabsf(A.z - B.z);
@@ -757,6 +764,9 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
                        const uint8_t* rep, const float* levels, int D, const int* vs, const int* sn, int aw,
                        float bl, int z0, int z1) {
   if (z1 <= z0) return 0;
+  // k_sweep_spixl's 32-bit byte offsets within a view (a re-laid one spans
+  // at most (W + H) H elements)
+  if ((long)(W + H) * H * 16 >= (1L << 31)) return arg_fail("superpixel sweep: image too large for 32-bit offsets");
   hipStream_t s = ctx->stream;
   int mw = map_dim(W, S), mh = map_dim(H, S);
   long M = (long)mw * mh;

@@ -495,6 +495,27 @@ def test_full_size_slic_properties(engine):
     assert_bits(lbh[0], olb, "1080p labels")
 
 
+@pytest.mark.parametrize("S", [32, 48, 64])
+@pytest.mark.parametrize("tiles9", ["0", "1"])
+def test_slic_tile_kernels(engine, monkeypatch, S, tiles9):
+    """The tile-fused assignment kernels against the oracle, labels and centres
+    bit for bit, on an image whose size is a multiple of neither 16 nor S:
+    k_assign_tiles4<S / 16> (S = 32, 64: the tile's four candidate cells,
+    branch-free distances, packed trees of the joined cells only) and the
+    9-cell k_assign_tiles (S = 48, whose tiles can straddle a candidate
+    boundary, or any S with MVS_SLIC_TILES9=1)."""
+    monkeypatch.setenv("MVS_SLIC_TILES9", tiles9)
+    W, H = 330, 250
+    stack, _ = synth.make_stack(W, H, 2, 1, 0, 15, 1.0, 31 + S)
+    lab, _ = engine.cvt(dev(stack))
+    sp, lb = engine.slic(lab, S, 0.6, 5)
+    sp, lb = sp.cpu().numpy(), as_u32(lb)
+    for v in range(2):
+        _, osp, olb = orc.slic(stack[v], S, 0.6, 5)
+        assert_bits(lb[v], olb, f"labels S={S} v{v}")
+        assert_bits(sp[v][..., :7], osp[..., :7], f"spixl S={S} v{v}")
+
+
 @pytest.mark.parametrize("kind", ["flat", "ramp", "checker"])
 def test_slic_ties(engine, kind):
     """Images built so that many pixels sit at (near-)equal distance from two
@@ -510,7 +531,7 @@ def test_slic_ties(engine, kind):
         img = np.where(((x // 8 + y // 8) % 2)[..., None] == 0, 40, 200).astype(np.uint8).repeat(3, -1)
     rgbx = np.concatenate([img, np.zeros((H, W, 1), np.uint8)], -1)[None]
     lab, _ = engine.cvt(dev(rgbx))
-    for S_ in (S, 32, 8):
+    for S_ in (S, 32, 8, 64):
         sp, lb = engine.slic(lab, S_)
         _, osp, olb = orc.slic(rgbx[0], S_)
         assert_bits(as_u32(lb)[0], olb, f"{kind} labels S={S_}")

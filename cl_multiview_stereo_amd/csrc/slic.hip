@@ -677,6 +677,7 @@ __global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
 
 // The same wave per tile for the reference's active 2x2 loop when S = 32 or
 // 64 (C2-C4's S = 32).  The tile's candidate cells are then the same four for
@@ -741,12 +742,17 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
     cbp[i >> 1][i & 1] = v[4];
   }
   const int lx = lane & 15, ly0 = lane >> 4;  // local index k = lane + 64*m, as the reference tile
+  // the tile's L, a, b as buffer loads: a pixel outside the image reads
+  // zeros (an offset past the view's records), with no branch around it
+  // (the launcher checks W H 16 < 2^31)
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)L, 0, (int)(P * 16), 0x00020000);
   float4 c[4];
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const int px = TX * 16 + lx, py = TY * 16 + ly0 + 4 * m;
     const bool in = px < W && py < H;
-    c[m] = in ? L[(long)py * W + px] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rl, in ? (py * W + px) * 16 : 0x7fffffff, 0, 0);
+    c[m] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), 0.f);
   }
   float cid[4];  // the candidates' labels as k_assign forms them
 #pragma unroll
@@ -1042,7 +1048,7 @@ int launch_assign_tiles(hipStream_t s, const float* lab, const float* spixl, int
   int ntx = (W + 15) / 16, nty = (H + 15) / 16;
   // MVS_SLIC_TILES9=1 (read per call): the 9-cell kernel for S % 32 == 0 too (A/B)
   const char* t9 = getenv("MVS_SLIC_TILES9");
-  if (!search && (S == 32 || S == 64) && !(t9 && atoi(t9) == 1))
+  if (!search && (S == 32 || S == 64) && (long)W * H * 16 < (1L << 31) && !(t9 && atoi(t9) == 1))
     hipLaunchKernelGGL(S == 32 ? k_assign_tiles4<2> : k_assign_tiles4<4>, dim3((ntx + 3) / 4, nty, V), dim3(256), 0,
                        s, (const float4*)lab, spixl, W, H, mw, mh, xy_n, col_n, weight, G, cpl, ntx, labels, part);
   else

@@ -757,6 +757,8 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
   float cid[4];  // the candidates' labels as k_assign forms them
 #pragma unroll
   for (int i = 0; i < 4; i++) cid[i] = (float)(ccy[i] * mw + ccx[i]);
+  const __amdgpu_buffer_rsrc_t rlb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(labels + (long)z * P), 0, (int)(P * 4), 0x00020000);
   uint32_t lbl[4];
   int win[4];  // the pixel's candidate (-1: none, or outside the image)
 #pragma unroll
@@ -825,10 +827,14 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
     const bool in = col < W && row < H;
     lbl[m] = in ? (uint32_t)min_id : 0xffffffffu;
     win[m] = in ? w : -1;
-    if (in) labels[(long)z * P + (long)row * W + col] = lbl[m];
+    // buffer stores throughout: a lane with nothing to store writes past the
+    // records (dropped), so no branch per store
+    __builtin_amdgcn_raw_buffer_store_b32(lbl[m], rlb, in ? (row * W + col) * 4 : 0x7fffffff, 0, 0);
   }
   if (!part) return;
   float* out = part + (long)z * mw * mh * G * 6;
+  const __amdgpu_buffer_rsrc_t rpt = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, mw * mh * G * 24, 0x00020000);
+  constexpr int kOob = 0x7fffffff;
   // the candidate cells some pixel of the tile joined (a wave-uniform mask)
   unsigned pres = 0;
 #pragma unroll
@@ -871,39 +877,43 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
     const float T2 = wave_tree2s(sa[1], sb[1]);                // lanes 0: a1, 32: b1
     const uint32_t Q = wave_sum2_u32(sq[0], sq[1]);            // lane 32 h: cell h's x, y, count
     const bool two = i1 != i0;
-    long base[2];
+    int base[2];  // (records of one view: the launcher checks the size)
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int i = h == 0 ? i0 : i1;
       const int gx = i == 0 ? ccx[0] : i == 1 ? ccx[1] : i == 2 ? ccx[2] : ccx[3];
       const int gy = i == 0 ? ccy[0] : i == 1 ? ccy[1] : i == 2 ? ccy[2] : ccy[3];
       const int t = (TY - (gy - 1) * s16) * cpl + (TX - (gx - 1) * s16);
-      base[h] = ((long)(gy * mw + gx) * G + t) * 6;
+      base[h] = ((gy * mw + gx) * G + t) * 6;
     }
     // each result stored from the lane holding it
-    if (lane == 0 || (lane == 32 && two)) {
+    {
       const int cnt = (Q >> 24) ? (int)(Q >> 24) : 256;  // present: at least one member
-      float* o = out + (lane == 0 ? base[0] : base[1]);
-      o[0] = (float)((int)(Q & 0xfffu) + cnt * 16 * TX);
-      o[1] = (float)((int)((Q >> 12) & 0xfffu) + cnt * 16 * TY);
-      o[5] = (float)cnt;
+      const bool qs = lane == 0 || (lane == 32 && two);
+      const int ob = qs ? (lane == 0 ? base[0] : base[1]) * 4 : kOob;
+      const float fx = (float)((int)(Q & 0xfffu) + cnt * 16 * TX), fy = (float)((int)((Q >> 12) & 0xfffu) + cnt * 16 * TY);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fx), rpt, ob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fy), rpt, qs ? ob + 4 : kOob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)cnt), rpt, qs ? ob + 20 : kOob, 0, 0);
+      const bool s1 = lane == 0 || lane == 16 || lane == 32 || (lane == 48 && two);
+      const int o1 = lane == 0 ? base[0] + 2 : lane == 16 ? base[0] + 4 : lane == 32 ? base[0] + 3 : base[1] + 2;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(T1), rpt, s1 ? o1 * 4 : kOob, 0, 0);
+      const bool s2 = two && (lane == 0 || lane == 32);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(T2), rpt, s2 ? (lane == 0 ? base[1] + 3 : base[1] + 4) * 4 : kOob,
+                                            0, 0);
     }
-    if (lane == 0 || lane == 16 || lane == 32 || (lane == 48 && two))
-      out[lane == 0 ? base[0] + 2 : lane == 16 ? base[0] + 4 : lane == 32 ? base[0] + 3 : base[1] + 2] = T1;
-    if (two && (lane == 0 || lane == 32)) out[lane == 0 ? base[1] + 3 : base[1] + 4] = T2;
   }
   // exact zeros for every other in-image cell of the 3x3 around the tile (no
   // pixel of the tile joined it): lane 6 j + ch, cell j
-  if (lane < 54) {
+  {
     const int j = lane / 6, ch = lane - 6 * j;
     const int gx = cxg - 1 + j % 3, gy = cyg - 1 + j / 3;
     bool joined = false;
 #pragma unroll
     for (int i = 0; i < 4; i++) joined = joined || (((joined_mask >> i) & 1u) && gx == ccx[i] && gy == ccy[i]);
-    if (!joined && gx >= 0 && gy >= 0 && gx < mw && gy < mh) {
-      const int t = (TY - (gy - 1) * s16) * cpl + (TX - (gx - 1) * s16);
-      out[((long)(gy * mw + gx) * G + t) * 6 + ch] = 0.0f;
-    }
+    const bool zw = lane < 54 && !joined && gx >= 0 && gy >= 0 && gx < mw && gy < mh;
+    const int t = (TY - (gy - 1) * s16) * cpl + (TX - (gx - 1) * s16);
+    __builtin_amdgcn_raw_buffer_store_b32(0u, rpt, zw ? (((gy * mw + gx) * G + t) * 6 + ch) * 4 : kOob, 0, 0);
   }
 }
 
@@ -1048,7 +1058,8 @@ int launch_assign_tiles(hipStream_t s, const float* lab, const float* spixl, int
   int ntx = (W + 15) / 16, nty = (H + 15) / 16;
   // MVS_SLIC_TILES9=1 (read per call): the 9-cell kernel for S % 32 == 0 too (A/B)
   const char* t9 = getenv("MVS_SLIC_TILES9");
-  if (!search && (S == 32 || S == 64) && (long)W * H * 16 < (1L << 31) && !(t9 && atoi(t9) == 1))
+  if (!search && (S == 32 || S == 64) && (long)W * H * 16 < (1L << 31) && (long)mw * mh * G * 24 < (1L << 31) &&
+      !(t9 && atoi(t9) == 1))
     hipLaunchKernelGGL(S == 32 ? k_assign_tiles4<2> : k_assign_tiles4<4>, dim3((ntx + 3) / 4, nty, V), dim3(256), 0,
                        s, (const float4*)lab, spixl, W, H, mw, mh, xy_n, col_n, weight, G, cpl, ntx, labels, part);
   else

@@ -87,11 +87,11 @@ def main():
         # views that pass's bench process swept (bench.py profile_counts)
         try:
             counts = json.load(open(os.path.join(src, "pmc_valu_bench.json")))["profile_counts"]
-            tot = sum(pmc[k]["SQ_INSTS_VALU_per_launch"] * pmc[k]["launches"] for k in ncc if k.endswith("true>"))
+            tot = sum(pmc[k]["SQ_INSTS_VALU_per_launch"] * pmc[k]["launches"] for k in ncc if ", true" in k)
             if counts.get("ncc_wta_views") and tot:
                 extra = {"fused_valu_wave_insts_per_view": tot / counts["ncc_wta_views"],
                          "fused_views_in_pass": counts["ncc_wta_views"],
-                         "fused_launches_in_pass": sum(pmc[k]["launches"] for k in ncc if k.endswith("true>"))}
+                         "fused_launches_in_pass": sum(pmc[k]["launches"] for k in ncc if ", true" in k)}
         except (OSError, ValueError, KeyError):
             pass
         json.dump({k: {"valu_wave_insts_per_launch": pmc[k]["SQ_INSTS_VALU_per_launch"],

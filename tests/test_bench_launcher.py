@@ -89,3 +89,18 @@ def test_sharded_subline_guard(mode):
         (line,) = _json_lines(p.stdout)
         assert line["value"] == 1.0 and "error" in line["view_sharded"]
         assert "returned" not in p.stdout
+
+
+@pytest.mark.parametrize("config", ["c2", "c5"])
+def test_committed_pmc_feeds_roofline_headline(config):
+    """The driver line's roofline_headline comes from the committed PMC summary
+    of the fused sweep (profiles/pmc_ncc_<config>.json, scripts/summarize_prof.py):
+    it must carry the per-view VALU count for the bench shape, and its source
+    must exist in the tree."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    cfg = bench.CONFIGS[config]
+    got = bench._valu_insts_fused_per_view(config, cfg["W"], cfg["H"], cfg["dmax"] - cfg["dmin"] + 1)
+    assert got is not None and got["insts"] > 0
+    assert os.path.exists(os.path.join(root, got["source"]))

@@ -182,6 +182,7 @@ def run(args):
 
 
 _WATCH = {"done": threading.Event(), "printed": False, "lock": threading.Lock()}
+WATCHDOG_EXIT = 3  # a hung sharded collective: the line is printed, the run still fails
 
 
 def _emit(res):
@@ -198,7 +199,8 @@ def _guarded_view_sharded(args, e, world, rank, sync, res):
     (async all-gathers, the point-to-point row exchange) run over RCCL -- a
     watchdog armed until the process is done prints the line without the field
     and ends the rank after MVS_SHARDED_TIMEOUT seconds (default 180) if they
-    hang, so every rank exits with the headline reported."""
+    hang: the headline is still reported, but the rank exits with status 3, so
+    a hung collective fails the run instead of passing as rc 0."""
     if world > 1:
         limit = float(os.environ.get("MVS_SHARDED_TIMEOUT", "180"))
 
@@ -209,8 +211,9 @@ def _guarded_view_sharded(args, e, world, rank, sync, res):
                 out = dict(res)
                 out["view_sharded"] = {"error": f"no result within {limit:.0f} s; rank exited by the bench watchdog"}
                 _emit(out)
-            log(f"rank {rank}: sharded sub-line watchdog fired after {limit:.0f} s")
-            os._exit(0)
+            log(f"rank {rank}: sharded sub-line watchdog fired after {limit:.0f} s; exiting with status 3")
+            sys.stdout.flush()
+            os._exit(WATCHDOG_EXIT)
 
         threading.Thread(target=watch, daemon=True).start()
     try:

@@ -153,7 +153,7 @@ void* scratch(mvs_ctx* ctx, size_t bytes, int* rc) {
 extern "C" {
 
 const char* mvs_last_error(void) { return g_err.c_str(); }
-const char* mvs_version(void) { return "mvs-mi355x 0.5 (gfx950)"; }
+const char* mvs_version(void) { return "mvs-mi355x 0.6 (gfx950)"; }
 
 int mvs_create(int device, mvs_ctx** out) {
   if (!out) return mvs::arg_fail("mvs_create: out is null");
@@ -311,9 +311,9 @@ int mvs_set_ncc_variant(mvs_ctx* c, int waves, int levels_per_wave, int band_w, 
   return 0;
 }
 
-int mvs_ncc_last_variant(mvs_ctx* c, int32_t* out7) {
-  if (!c || !out7) return mvs::arg_fail("mvs_ncc_last_variant: null argument");
-  for (int i = 0; i < 7; i++) out7[i] = c->ncc_last[i];
+int mvs_ncc_last_variant(mvs_ctx* c, int32_t* out8) {
+  if (!c || !out8) return mvs::arg_fail("mvs_ncc_last_variant: null argument");
+  for (int i = 0; i < 8; i++) out8[i] = c->ncc_last[i];
   return 0;
 }
 

@@ -32,7 +32,7 @@ struct mvs_ctx {
   // NCC sweep variant override (mvs_set_ncc_variant; 0 = automatic) and the
   // variant of the last launch {K, TH, DPW, NW, BW, EVEN, FUSE}
   int ncc_nw = 0, ncc_dpw = 0, ncc_bw = 0, ncc_general = 0;
-  int ncc_last[7] = {0, 0, 0, 0, 0, 0, 0};
+  int ncc_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 namespace mvs {

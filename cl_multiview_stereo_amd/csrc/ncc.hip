@@ -745,8 +745,8 @@ template <int K, int TH, int DPW, int NW, int BW, int PAR, int NB = 2>
 int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRec* plan, NccArgs& a, float* vol,
                   const WtaOut& wo, size_t lds) {
   hipStream_t s = ctx->stream;
-  const int variant[7] = {K, TH, DPW, NW, BW, PAR, vol ? 0 : 1};
-  std::copy(variant, variant + 7, ctx->ncc_last);
+  const int variant[8] = {K, TH, DPW, NW, BW, PAR, vol ? 0 : 1, NB};
+  std::copy(variant, variant + 8, ctx->ncc_last);
   constexpr int DC = NW * DPW;
   a.tiles_x = (a.W + 63) / 64;
   a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);

@@ -225,9 +225,12 @@ class Engine:
                                               int(bool(general_rows))), "mvs_set_ncc_variant")
 
     def ncc_last_variant(self) -> dict:
-        v = (C.c_int32 * 7)()
+        """The last NCC launch: K, tile rows, levels per wave, waves, band width,
+        PAR (row parity: 0 mixed, 1 every band row pair-aligned, 2 odd pk / even
+        stats rows), FUSE, NB (band buffers: 1 single, 2 double)."""
+        v = (C.c_int32 * 8)()
         _lib.check(self.L.mvs_ncc_last_variant(self.ctx, v), "mvs_ncc_last_variant")
-        return dict(zip(("K", "TH", "DPW", "NW", "BW", "EVEN", "FUSE"), list(v)))
+        return dict(zip(("K", "TH", "DPW", "NW", "BW", "PAR", "FUSE", "NB"), list(v)))
 
     def ncc_volume(self, l8, box, cam: CameraArray, z: int, K: int = 5, out=None):
         V, H, W = l8.shape

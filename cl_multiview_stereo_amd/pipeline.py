@@ -139,11 +139,11 @@ class Pipeline:
     concurrent=True: after the colour conversion the superpixel chain (SLIC,
     extents, superpixel sweep: latency/L2-bound gathers) runs on a second HIP
     stream with its own libmvs context, beside the per-pixel chain (window
-    planes, NCC volume, WTA: VALU- and HBM-bound) on the caller's stream; the
-    caller's stream joins the side stream before refinement.  Measured at C2:
-    1 % more Mpix/s, the NCC kernel 0.42 -> 0.56 ms while it shares the GPU
-    and the WTA pass 0.73 -> 0.70 of the HBM roofline, so it is off by
-    default (bench.py --concurrent)."""
+    planes, fused NCC sweep + WTA) on the caller's stream; the caller's stream
+    joins the side stream before refinement.  bench.py makes it the default
+    for the unsharded fused-NCC configurations (--serial turns it off); the
+    class default stays False so library callers get one stream unless they
+    ask for the second."""
 
     def __init__(self, engine: Engine, settings: params.Settings, W: int, H: int,
                  view_subset: list[list[int]] | None = None, pixel_cost: str | None = "ncc",

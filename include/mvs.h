@@ -183,9 +183,10 @@ int mvs_ncc_wta_range_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int
  * on a pair.  Variants that do not fit the LDS fall back as in the default
  * chain.  mvs_ncc_last_variant reports the last launch as
  * {K, TH, levels per wave, waves, band width, row parity (0 mixed, 1 every band
- * row pair-aligned, 2 every pk row odd and stats row even), fused}. */
+ * row pair-aligned, 2 every pk row odd and stats row even), fused, band buffers
+ * (1 single-buffered, 2 double-buffered)}: eight int32. */
 int mvs_set_ncc_variant(mvs_ctx* ctx, int waves, int levels_per_wave, int band_w, int general_rows);
-int mvs_ncc_last_variant(mvs_ctx* ctx, int32_t* out7);
+int mvs_ncc_last_variant(mvs_ctx* ctx, int32_t* out8);
 
 /* Superpixel-plane refinement (clDepthRefinement, depth_refinement.cpp:91-1470).
  * flat [V][mh][mw][2] and state/state2 [V][mh][mw][6] are caller-provided

@@ -77,18 +77,65 @@ bench._WATCH["done"].set()
 def test_sharded_subline_guard(mode):
     """The C4 sub-line at world > 1 cannot take the headline line with it: an
     exception comes back as {"error": ...}; a hang trips the watchdog, which
-    prints the line without the field and ends the rank with status 0."""
+    prints the line without the field and ends the rank with status 3 (a hung
+    collective must fail the run, never pass as rc 0)."""
     env = _env()
     env["MVS_SHARDED_TIMEOUT"] = "2"
     p = subprocess.run([sys.executable, "-c", _GUARD.format(root=ROOT, mode=mode)], env=env, capture_output=True,
                        text=True, timeout=120)
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == (0 if mode == "raise" else 3), p.stderr
     if mode == "raise":
         assert "returned {'error': \"RuntimeError('collective failed')\"}" in p.stdout
     else:
         (line,) = _json_lines(p.stdout)
         assert line["value"] == 1.0 and "error" in line["view_sharded"]
         assert "returned" not in p.stdout
+
+
+_HANG = """
+import os, sys, time
+sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+import bench
+from cl_multiview_stereo_amd.distributed import ViewGather
+dist.init_process_group("gloo")
+rank = dist.get_rank()
+
+def vs(args, e, world, rank, sync):
+    # the sharded leg's own all-gather; rank 1 never joins it, so rank 0's
+    # collective hangs inside gloo exactly as a stuck RCCL gather would
+    g = ViewGather(4)
+    full = torch.zeros((4, 8))
+    z0, z1 = g.block
+    if rank == 1:
+        time.sleep(120)
+    g(full[z0:z1], full)
+    return {{"ok": True}}
+
+bench.view_sharded = vs
+r = bench._guarded_view_sharded(None, None, 2, rank, None, {{"metric": "m", "value": 1.0}})
+print("returned", r, flush=True)
+"""
+
+
+def test_hung_collective_fails_the_run(tmp_path):
+    """A gloo world-2 job whose sharded leg hangs in a real all-gather (rank 1
+    never joins): the watchdog prints the headline line on rank 0 with the
+    sharded field set to an error, and the job exits non-zero."""
+    script = tmp_path / "hang.py"
+    script.write_text(_HANG.format(root=ROOT))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = _env()
+    env["MVS_SHARDED_TIMEOUT"] = "3"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode != 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["value"] == 1.0 and "error" in line["view_sharded"]
+    assert "returned" not in r.stdout
 
 
 @pytest.mark.parametrize("config", ["c2", "c5"])

@@ -135,7 +135,7 @@ def test_c4_geometry(eng, bl, nb, monkeypatch):
         od, oc = orc.wta(want, cam.levels)
         vol = eng.ncc_volume(l8, box, cam, z, 5)
         v = eng.ncc_last_variant()
-        variants.add((v["DPW"], v["NW"], v["BW"], v["EVEN"]))
+        variants.add((v["DPW"], v["NW"], v["BW"], v["PAR"], v["NB"]))
         same(vol, want, f"volume z{z}")
         d, c = eng.wta(vol, eng.levels_dev(cam))
         same(d, od, f"disp z{z}")
@@ -146,8 +146,11 @@ def test_c4_geometry(eng, bl, nb, monkeypatch):
     dpws = {v[0] for v in variants}
     if nb == "1":  # every list but the corner views' (a neighbour two rows away) takes 32-level chunks
         assert 4 in dpws, f"single-buffered 32-level chunks expected, saw {sorted(variants)}"
+        # the single-buffered kernel ran, seen directly (NB slot), for the mixed-parity 5-NN lists
+        assert any(v[4] == 1 for v in variants), f"single-buffered bands expected, saw {sorted(variants)}"
     else:
         assert dpws & {1, 2}, f"C4 geometry should need a narrower variant, saw {sorted(variants)}"
+        assert {v[4] for v in variants} == {2}, f"MVS_NCC_NB=2 must keep double buffers, saw {sorted(variants)}"
 
 
 _VARIANTS = [(8, 4), (8, 2), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation
@@ -193,8 +196,8 @@ def test_every_ncc_variant(eng, K, geom):
                 assert v["BW"] == max(bw, need), (tag, v)
                 seen.add(v["BW"])
                 if general:
-                    assert v["EVEN"] == 0, (tag, v)
-                evens.add(v["EVEN"])
+                    assert v["PAR"] == 0, (tag, v)
+                evens.add(v["PAR"])
                 same(vol, want, f"volume {tag}")
                 fd, fc = eng.ncc_wta(l8, box, cam, z, K)
                 v = eng.ncc_last_variant()

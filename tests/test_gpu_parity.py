@@ -400,17 +400,15 @@ def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns, bound):
     assert_bits(out.cpu().numpy(), oout, f"filter output ({kern}, FB {fb})")
 
 
-@pytest.mark.parametrize("kern", ["q", "px"])
-@pytest.mark.parametrize("aw,ah", [(3, 2), (4, 3), (8, 4), (9, 5), (10, 7)])
+@pytest.mark.parametrize("kern,aw,ah", [("q", 3, 2), ("q", 4, 3), ("q", 8, 4), ("q", 9, 5), ("q", 10, 7),
+                                         ("px", 8, 4)])
 def test_filter_row_bands(engine, monkeypatch, aw, ah, kern):
     # mvs_proj_inv_rows_d / mvs_remove_inconsistency_rows_d (the sharded
     # pipeline's banded proj all-gather): uneven row bands, every band written
     # into shared proj / out buffers, tile the full-range result for every
     # removal kernel (V = 6, 12, 32, 45, 70; the 16 < V <= 32 kernels forced
     # per call), the projection into the full stack and into band buffers
-    V, H, W = aw * ah, 23, 70
-    if kern != "q" and V != 32:
-        pytest.skip("removal kernel variants apply at 16 < V <= 32")
+    V, H, W = aw * ah, 23, 70  # the "px" removal variant is forced only at 16 < V <= 32 (8 x 4)
     rng = np.random.default_rng(aw * 13 + ah)
     base = rng.integers(2, 9, size=(V, 1, 1)).astype(np.float32)
     disp = base + rng.choice(np.float32([0.0, 0.5, 1.0, 3.0]), size=(V, H, W))

@@ -65,6 +65,10 @@ CONFIGS = {
 METRIC = "Mpix/s depth (1080p, 128 depth hyp, 5 views) + depth L1 vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK = 1024 * 2.4e9 / 4.0  # wave64 VALU instructions/s: 1024 SIMDs x 2.4 GHz / 4 cycles
+VALU_PEAK_NOTE = ("1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction: profiles/r05/valu_rate3.txt measures "
+                  "v_dot4_i32_i8 / v_pk_fma_f32 / v_pk_mul_f32 / v_max_f32 / v_med3_f32 at 4.13-4.35 cycles per "
+                  "wave-instruction per SIMD at 4-8 waves per SIMD (v_add_f32 / v_mul_f32 / v_mov_b32 2.2-2.5, "
+                  "v_fma_f32 3.6-3.8); the sweep's mix weighs in at ~3.9")
 CPU_SAMPLE_SECONDS = 15.0  # target CPU time of the per-pixel sweep's sampled row band (cpu_baseline)
 CPU_TAP_RATE = {"ncc": 13e9, "sad": 8e9}  # oracle taps/s on the GPU box's 16 host threads (measured r02)
 
@@ -85,6 +89,8 @@ def parse(argv=None):
     ap.add_argument("--no-reference-cost", action="store_true", help="skip the C2 --cost sad sub-line")
     ap.add_argument("--no-reference-defaults", action="store_true",
                     help="skip the `reference_defaults` sub-line (--config ref inside the c2 line)")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the `c3` sub-line (--config c3: refinement + consistency filter, inside the c2 line)")
     ap.add_argument("--two-pass", action="store_true",
                     help="headline = the two-pass step (cost volume in HBM + k_wta) instead of the fused sweep")
     ap.add_argument("--concurrent", action="store_true",
@@ -312,16 +318,28 @@ def _valu_insts(name, cost, fused, W, H, D):
 
 def _valu_insts_fused_per_view(name, W, H, D):
     """SQ_INSTS_VALU of the fused sweep per reference view: the PMC pass's
-    total over every FUSE=true launch divided by the reference views its bench
+    total over every fused launch divided by the reference views its bench
     process swept (profile_counts.ncc_wta_views of that run's own JSON line,
-    recorded by scripts/summarize_prof.py as fused_valu_wave_insts_per_view)."""
+    recorded by scripts/summarize_prof.py as fused_valu_wave_insts_per_view).
+    "stale" is set when the NCC sources changed since that pass (the summary
+    records their hash), so no fraction is quoted on another kernel's counts."""
     p = os.path.join(ROOT, "profiles", f"pmc_ncc_{name}.json")
     if not os.path.exists(p):
         return None
     j = json.load(open(p))
     if (j.get("W"), j.get("H"), j.get("D")) != (W, H, D) or "fused_valu_wave_insts_per_view" not in j:
         return None
-    return {"insts": j["fused_valu_wave_insts_per_view"], "source": j.get("source")}
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from summarize_prof import ncc_src_sha16
+    now = ncc_src_sha16(ROOT)
+    kern = next((k for k in j if k.startswith("k_ncc_mfma")), None) or next(
+        (k for k in j if k.startswith("k_ncc_volume") and ", true" in k), "k_ncc_volume<..., FUSE=true>")
+    out = {"insts": j["fused_valu_wave_insts_per_view"], "source": j.get("source"),
+           "mfma": j.get("fused_mfma_insts_per_view", 0.0), "kernel": kern}
+    if j.get("ncc_src_sha16") != now:
+        out["stale"] = (f"the PMC pass ({j.get('source')}) counted NCC sources {j.get('ncc_src_sha16')}, this tree "
+                        f"is {now}: no fraction quoted until scripts/profile.sh is re-run")
+    return out
 
 
 def bench(args, world, rank, local):
@@ -410,6 +428,7 @@ def bench(args, world, rank, local):
     units = V if sharded else world * V  # reference views processed per step, whole job
     mpix = units * W * H * args.steps / elapsed / 1e6
     head_timers = {k: list(v) for k, v in timers.items()}
+    form_timers = head_timers  # the headline's own form (side stream included): roofline_headline
     serial = None
     if conc_head:
         # the same step on one stream: the fused kernel's own time for
@@ -464,28 +483,45 @@ def bench(args, world, rank, local):
         nbr = max(1, int(pipe.cam.subset_num[0]))
         per_view = _valu_insts_fused_per_view(args.config, W, H, D)
         res["roofline_sweep"] = {
-            "kernel": "k_ncc_volume<..., FUSE=true> (fused sweep + WTA, the headline step's dominant kernel)",
+            "kernel": "fused sweep + WTA (k_ncc_mfma for K = 5 horizontal lists, else k_ncc_volume<..., FUSE=true>): the headline step's dominant kernel",
             "bound": "valu", "avg_call_ms": round(t_f * 1e3, 4), "views_per_call": vpc,
             "avg_ms_per_view": round(t_f * 1e3 / vpc, 4),
             "view_cells_per_s": round(cells * nbr * vpc / t_f / 1e9, 3), "unit_view_cells": "G view-cells/s",
             "timing": "HIP events around each mvs_ncc_wta_range_d call of the timed steps, on its stream" +
                       (" (the serial_variant pass: one stream, the kernel alone on the GPU)" if conc_head else "")}
-        if per_view is not None:
+        if per_view is not None and not per_view.get("stale"):
             res["roofline_sweep"].update({
                 "valu_wave_insts_per_view": round(per_view["insts"]),
                 "valu_issue_frac": round(per_view["insts"] * vpc / t_f / VALU_PEAK, 4),
-                "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 op",
+                "valu_peak": VALU_PEAK_NOTE,
                 "valu_source": per_view["source"]})
-            # the roofline of the kernel the headline step actually spends its time in
-            ach = per_view["insts"] * vpc / t_f / 1e9
-            res["roofline_headline"] = {
-                "bound": "valu", "kernel": "k_ncc_volume<..., FUSE=true> (fused sweep + WTA)",
-                "achieved": round(ach, 1), "peak": round(VALU_PEAK / 1e9, 1), "unit": "G VALU wave-instr/s",
-                "frac": round(ach * 1e9 / VALU_PEAK, 4),
-                "algorithmic": f"{round(per_view['insts'])} VALU wave-instructions per reference view "
-                               f"(SQ_INSTS_VALU of its own PMC pass, {per_view['source']}) over the HIP-event "
-                               f"time per view of the serial pass",
-                "avg_ms_per_view": round(t_f * 1e3 / vpc, 4)}
+        if per_view is not None:
+            # the roofline of the kernel the headline step spends its time in,
+            # timed in the headline's own form (side stream beside it) and, for
+            # reference, alone on one stream (the serial pass)
+            def form(tm):
+                tf = avg(tm["fused"])
+                vp = sum(n for _, _, n in tm["fused"]) / len(tm["fused"])
+                return tf, vp
+            t_h, v_h = form(form_timers) if form_timers["fused"] else (t_f, vpc)
+            issue = per_view["insts"] + 2.0 * per_view.get("mfma", 0.0)  # an MFMA holds VALU issue for 8 cycles
+            ach = issue * v_h / t_h / 1e9
+            rh = {"bound": "valu", "kernel": per_view["kernel"],
+                  "achieved": round(ach, 1), "peak": round(VALU_PEAK / 1e9, 1), "unit": "G VALU wave-instr/s",
+                  "frac": round(ach * 1e9 / VALU_PEAK, 4),
+                  "form": "headline (superpixel chain on the side stream)" if conc_head else "headline (one stream)",
+                  "algorithmic": f"{round(per_view['insts'])} VALU wave-instructions per reference view"
+                                 + (f" + 2 x {round(per_view['mfma'])} MFMA (8 issue cycles each)"
+                                    if per_view.get("mfma") else "")
+                                 + f" (SQ_INSTS_VALU of its own PMC pass, {per_view['source']}) over the HIP-event "
+                                   f"time per view of the headline pass",
+                  "avg_ms_per_view": round(t_h * 1e3 / v_h, 4), "peak_basis": VALU_PEAK_NOTE}
+            if conc_head:
+                rh["serial_form"] = {"avg_ms_per_view": round(t_f * 1e3 / vpc, 4),
+                                     "frac": round(issue * vpc / t_f / VALU_PEAK, 4)}
+            if per_view.get("stale"):
+                rh.update({"frac": None, "achieved": None, "stale_pmc": per_view["stale"]})
+            res["roofline_headline"] = rh
 
     # the two-pass step (cost volume in HBM + k_wta), same protocol: the
     # north star's roofline is k_wta's read of that volume
@@ -562,6 +598,14 @@ def bench(args, world, rank, local):
                                                            check=rank == 0 and not args.no_cpu_baseline)
         except Exception as ex:  # report, never hide; the headline stands
             res["reference_defaults"] = {"error": repr(ex)}
+
+    # BASELINE config 3 (C2 + refinement + consistency filter) inside the default
+    # line, its refined and filtered maps against the oracle's full-size run
+    if args.config == "c2" and cost == "ncc" and world == 1 and not args.no_c3:
+        try:
+            res["c3"] = c3_subline(args, e, world, sync, check=rank == 0 and not args.no_cpu_baseline)
+        except Exception as ex:  # report, never hide; the headline stands
+            res["c3"] = {"error": repr(ex)}
 
     # C4: one 32-view array sharded by reference view over the N GPUs (strong scaling)
     if not args.no_sharded and args.config in ("c2",) and cost == "ncc":
@@ -644,6 +688,62 @@ def reference_defaults(args, e, world, sync, check=True):
         cpu, l1 = cpu_baseline(p, stack, c, "none", out)
         r["depth_l1_vs_oracle"] = l1
         r["cpu_baseline"] = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")}
+    return r
+
+
+def c3_subline(args, e, world, sync, check=True):
+    """`--config c3` inside the default line: the C2 step + superpixel
+    refinement (5 propagations, fusion) + the cross-view consistency filter
+    (project_to_reference_inv + remove_view_inconsistency, clcode.cl:1995-2101),
+    5 views 1920x1080, with the headline's stream layout (superpixel chain on
+    the side stream).  5 timed steps after 1 warmup; with `check`, the last
+    step's refined and filtered maps (and labels, seeds) against the oracle's
+    full-size run (segmentation, superpixel sweep, refinement, filter: ~3 s on
+    the host; the per-pixel NCC maps are the headline's, checked there)."""
+    import torch
+
+    from cl_multiview_stereo_amd import params, synth
+    from cl_multiview_stereo_amd.pipeline import Pipeline
+    c = CONFIGS["c3"]
+    V, W, H, S = c["aw"] * c["ah"], c["W"], c["H"], c["S"]
+    st = params.Settings(spixl_size=S, array_width=c["aw"], array_height=c["ah"], min_disp=c["dmin"],
+                         max_disp=c["dmax"], inc=1, neib_hor=c["nh"], neib_ver=c["nv"], bl_ratio=c["bl"],
+                         window=c["K"], cost="ncc")
+    stack, _ = synth.make_stack(W, H, c["aw"], c["ah"], c["dmin"], c["dmax"], c["bl"], 0x5EED + 2)  # = --config c3
+    rgbx = torch.from_numpy(stack).to(e.device)
+    p = Pipeline(e, st, W, H, pixel_cost="ncc", refine=True, filt=True, concurrent=not args.serial, fused=True)
+    steps = 5
+    el, out = timed(lambda: p.exe_pipeline(rgbx), steps, 1, e.device, world, sync)
+    r = {"what": c["workload"], "value": round(V * W * H * steps / el / 1e6, 3), "unit": "Mpix/s",
+         "ms_per_step": round(el * 1e3 / steps, 4), "steps": steps,
+         "streams": "one" if args.serial else "superpixel chain on a side stream"}
+    if check:
+        from oracle import oracle as orc
+        t0 = time.perf_counter()
+        cam = p.cam
+        outs = [orc.slic(stack[v], S) for v in range(V)]
+        lab = np.stack([o[0] for o in outs])
+        sp = np.stack([o[1] for o in outs])
+        lb = np.stack([o[2] for o in outs])
+        rep = orc.boundary(sp, lb, S)
+        sp = orc.sweep(lab, sp, rep, cam.levels, cam.view_subset, cam.subset_num, c["aw"], c["bl"], S)
+        ref = orc.refine(sp, lb, rep, cam.view_subset, cam.subset_num, c["aw"], c["bl"], S)["disp"]
+        filt = orc.filt(ref, c["aw"], c["bl"], 1.0)[1]
+        t_orc = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        maps = {"labels": (out.labels.cpu().numpy().view(np.uint32), lb), "spixl": (out.spixl.cpu().numpy(), sp),
+                "disp_refined": (out.disp_refined.cpu().numpy(), ref),
+                "disp_filtered": (out.disp_filtered.cpu().numpy(), filt)}
+        l1 = {}
+        for k, (g, w) in maps.items():
+            l1[k] = {"bit_exact": bool(np.array_equal(g, w))}
+            if k.startswith("disp"):
+                l1[k]["value"] = float(np.abs(g - w).mean())
+        r["depth_l1_vs_oracle"] = {"value": l1["disp_filtered"]["value"], "unit": "px (mean |d_gpu - d_oracle|)",
+                                   "bit_exact": all(v["bit_exact"] for v in l1.values()), "map": "disp_filtered",
+                                   "maps": l1,
+                                   "sample": f"the last timed step, all {V} views {W}x{H} (oracle: {t_orc:.1f} s on "
+                                             f"the host)"}
     return r
 
 

@@ -30,7 +30,7 @@ struct mvs_ctx {
   // per distinct content and kept for the life of the context
   std::map<std::vector<int32_t>, int32_t*> plans;
   // NCC sweep variant override (mvs_set_ncc_variant; 0 = automatic) and the
-  // variant of the last launch {K, TH, DPW, NW, BW, EVEN, FUSE}
+  // variant of the last launch {K, TH, DPW, NW, BW, PAR, FUSE, NB} (DPW 16: the matrix-core form)
   int ncc_nw = 0, ncc_dpw = 0, ncc_bw = 0, ncc_general = 0;
   int ncc_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };

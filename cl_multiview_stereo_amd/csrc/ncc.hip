@@ -45,17 +45,12 @@
 #include <type_traits>
 #include <cstdlib>
 
-#include "mvs_internal.h"
+#include "ncc_common.h"
 
 namespace mvs {
 namespace {
+using namespace ncc;
 
-// Row-pair interleaved planes: element (y, x) of a view lives at uint2 index
-// ((y >> 1) * W + x) * 2 + (y & 1), over Hp = H rounded up to even rows, so
-// one 16-byte access returns rows 2m and 2m+1 of one column.
-__host__ __device__ __forceinline__ long pair_index(int y, int x, int W) {
-  return (((long)(y >> 1) * W + x) << 1) + (y & 1);
-}
 
 // ---- window statistics + packed intensities ------------------------------
 // one workgroup = 64 columns x 16 rows of one view; the (16+2R) x 76 byte
@@ -151,150 +146,6 @@ __global__ __launch_bounds__(256) void k_box_stats(const uint8_t* __restrict__ q
   }
 }
 
-constexpr int kMaxNbr = 16;
-constexpr int kMaxRef = 8;  // reference views per launch (the fused sweep takes a run of them)
-constexpr int kCPolNT = 2;  // buffer cache policy: non-temporal (CPol::NT on gfx940+)
-struct NccArgs {
-  int W, H, D, nref;
-  int tiles_x, ntiles, tiles_per_xcd, nch;  // XCD-aware work map over nref x ntiles tiles (see k_ncc_volume)
-  int pk_pairs, st_pairs;  // LDS band heights in row pairs; the pair-row stride is the template BW
-  // per reference view r of the launch: view id, neighbour count, first plan
-  // record, neighbour view ids
-  int z[kMaxRef], nn[kMaxRef], plan[kMaxRef];
-  int view[kMaxRef][kMaxNbr];
-};
-// host-built plan (device memory, cached per context): one 128-B record per
-// (chunk c, neighbour n, wave w), read with one scalar load per neighbour.
-// A __restrict__ kernel parameter, so the loads are SMEM and never wait on
-// the vector-memory counter the LDS-DMA prefetch runs under.
-struct alignas(128) NccRec {
-  int txmax, tymax;  // band origin: image column x0 - txmax; pk pair (y0-R-tymax)>>1, stats pair (y0-tymax)>>1
-  int bhp, shp;      // pk pair rows to stage, stats pair rows | (64-px blocks per row) << 16
-  int lv[16];        // per level j of wave w: {txmax - tx, pk start row | stats start row << 16 (band-relative)}
-  int pad[12];
-};
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gptr_t;
-// 16-byte LDS-DMA: lane l's 16 bytes land at dst + 16*l (dst wave-uniform)
-__device__ __forceinline__ void glds_b128(const void* src, void* dst) {
-  __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
-}
-
-// v_max_f32 (IEEE maxNum: a quiet-NaN operand is dropped).  Inline asm so the
-// compiler does not re-canonicalise the loop-carried accumulators every pass.
-__device__ __forceinline__ float vmax(float acc, float e) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(e));
-  return r;
-}
-// max(-1, e) with -1.0 as an inline constant (no VGPR holding it)
-__device__ __forceinline__ float vmax_m1(float e) {
-  float r;
-  asm("v_max_f32 %0, -1.0, %1" : "=v"(r) : "v"(e));
-  return r;
-}
-__device__ __forceinline__ float vmin(float acc, float e) {
-  float r;
-  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(e));
-  return r;
-}
-// median of three: with lo <= hi, med3(lo, hi, c) = min(hi, max(lo, c))
-__device__ __forceinline__ float vmed3(float lo, float hi, float c) {
-  float r;
-  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(lo), "v"(hi), "v"(c));
-  return r;
-}
-
-// Fused winner-take-all outputs (k_ncc_volume<..., FUSE = true>): the volume
-// is never written.  Same results as k_wta over the materialised volume.
-struct WtaOut {
-  const float* levels;  // device [D]
-  float* disp;          // [H][W]
-  float* conf;          // [H][W] or null
-};
-constexpr float kWtaInit = 1000000.0f;  // k_wta's Top4 initial cost (sweep.hip)
-
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-// Row-parity modes of a launch's bands (k_ncc_volume's PAR; the plan knows it):
-//   kParEven  every level's pk and stats rows start on a pair boundary (K = 5
-//             with horizontal neighbours: R + tymax even)
-//   kParOdd   every pk start is odd and every stats start even (K = 7 with
-//             horizontal neighbours: R = 3)
-//   kParMixed either, per level (vertical / diagonal neighbours): a run-time test
-constexpr int kParMixed = 0, kParEven = 1, kParOdd = 2;
-
-// N consecutive band rows starting at band row r0 of a row-pair band (pair
-// row stride BW, one column): ds_read_b128 per pair; an odd start takes the
-// first and last rows as ds_read_b64 halves.  N even.
-template <int N, int BW, int PAR>
-__device__ __forceinline__ void read_rows(const u32x4* col, int r0, u32x2 (&v)[N]) {
-  const u32x4* p = col + (r0 >> 1) * BW;
-  if (PAR == kParEven || (PAR == kParMixed && (r0 & 1) == 0)) {
-#pragma unroll
-    for (int i = 0; i < N / 2; i++) {
-      const u32x4 t = p[i * BW];
-      v[2 * i] = t.xy;
-      v[2 * i + 1] = t.zw;
-    }
-  } else {
-    v[0] = ((const u32x2*)p)[1];
-#pragma unroll
-    for (int i = 1; i < N / 2; i++) {
-      const u32x4 t = p[i * BW];
-      v[2 * i - 1] = t.xy;
-      v[2 * i] = t.zw;
-    }
-    v[N - 1] = ((const u32x2*)(p + (N / 2) * BW))[0];
-  }
-}
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// The N/2 stats row pairs (o, o+1), o even, of a band column starting at band
-// row r0: {a(o), a(o+1), b(o), b(o+1)}.  An odd start joins the second row of
-// one stored pair with the first row of the next.
-template <int N, int BW, int PAR>
-__device__ __forceinline__ void read_stat_pairs(const u32x4* col, int r0, f32x4 (&v)[N / 2]) {
-  const u32x4* p = col + (r0 >> 1) * BW;
-  if (PAR != kParMixed || (r0 & 1) == 0) {
-#pragma unroll
-    for (int i = 0; i < N / 2; i++) v[i] = __builtin_bit_cast(f32x4, p[i * BW]);
-  } else {
-    // only the 16 needed dwords, as ds_read2_b32 pairs ({a, b} of one stored
-    // row): no stored pair held whole, so the odd path needs no more registers
-    // than the even one (the whole-pair form kept N/2 + 1 pairs live, and the
-    // fused mixed-parity kernels spilled their fold accumulators for it)
-    const float* f = (const float*)p;
-#pragma unroll
-    for (int i = 0; i < N / 2; i++) {
-      const float* q0 = f + i * BW * 4;        // stored pair i: second rows (y, w)
-      const float* q1 = f + (i + 1) * BW * 4;  // stored pair i + 1: first rows (x, z)
-      v[i] = f32x4{q0[1], q1[0], q0[3], q1[2]};
-    }
-  }
-}
-
-// v_dot4_i32_i8 is the VOP3P form (separate destination): a prefix-sum chain
-// keeps every partial sum without the accumulator copies the VOP2 v_dot4c
-// form forces.  The Makefile builds this file with the dot6 feature (v_dot4c)
-// off, so the compiler selects the VOP3P form and still tracks its hazards.
-// the lane id, recomputed where it is used (volatile: never hoisted, so it is
-// never a long-lived value the register allocator would spill)
-__device__ __forceinline__ int lane_now() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
-
-constexpr int kMagicI = 0x4B400000;  // the bits of 12582912.0f = 1.5 * 2^23
-constexpr float kMagicF = 12582912.0f;
-__device__ __forceinline__ int dot4(unsigned a, unsigned b, int c) {
-  return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
-}
 
 // PAR: the bands' row parity (kParEven / kParOdd: branch-free pair reads).
 // FUSE: instead of writing the volume, every wave folds its levels' costs into
@@ -916,17 +767,35 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   if (n <= 0) return 0;
   std::vector<NccChoice> ch(n);
   std::vector<std::array<int, kMaxNbr>> views(n);
+  // the matrix-core form (k_ncc_mfma) for fused K = 5 views whose neighbours
+  // are all horizontal (every vertical shift 0) and whose bands leave two
+  // workgroups per CU; MVS_NCC_MFMA=0 (read per call) or a forced variant
+  // (mvs_set_ncc_variant) keeps the scalar kernels
+  const char* mfe = getenv("MVS_NCC_MFMA");
+  const bool mf_on = !vol && K == 5 && !(mfe && atoi(mfe) == 0) && !ctx->ncc_nw && !ctx->ncc_dpw && !ctx->ncc_general &&
+                     !ctx->ncc_bw;
+  std::vector<char> mf(n, 0);
+  std::vector<NccPlanM> mplan(n);
   for (int r = 0; r < n; r++) {
     const int z = z0 + r, nn = sn_host[z];
     if (nn > kMaxNbr) return arg_fail("NCC sweep supports at most 16 neighbours per reference view");
     float fdx[kMaxNbr], fdy[kMaxNbr];
     const int rx = z % aw, ry = z / aw;
+    bool horiz = true;
     for (int k = 0; k < nn; k++) {
       const int v = vs_host[V * z + k];
       if (v < 0 || v >= V) return arg_fail("view_subset entry out of range");
       views[r][k] = v;
       fdx[k] = (float)(v % aw - rx);
       fdy[k] = (float)(v / aw - ry);
+      if (fdy[k] != 0.0f) horiz = false;
+    }
+    if (mf_on && horiz && nn > 0) {
+      mplan[r] = make_plan_mfma(levels_host, D, nn, fdx);
+      if (mplan[r].band_w <= 192) {
+        mf[r] = 1;
+        continue;
+      }
     }
     const bool ok = K == 5 ? choose_variant<5>(ctx, levels_host, D, nn, fdx, fdy, bl, ch[r])
                            : choose_variant<7>(ctx, levels_host, D, nn, fdx, fdy, bl, ch[r]);
@@ -940,11 +809,42 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   const char* re = getenv("MVS_NCC_RUN");
   const int maxrun = re ? std::max(1, std::min(kMaxRef, atoi(re))) : kMaxRef;
   for (int i = 0; i < n;) {
+    if (mf[i]) {  // a run of matrix-core views: one launch, the widest band
+      int j = i, bw = 0, tmax = 0;
+      NccArgs a{};
+      a.W = W;
+      a.H = H;
+      a.D = D;
+      a.pk_pairs = 6;
+      a.st_pairs = 4;
+      std::vector<int32_t> table;
+      while (j < n && mf[j] && j - i < maxrun) {
+        const int z = z0 + j;
+        bw = std::max(bw, mplan[j].band_w);
+        tmax = std::max(tmax, ((D + 31) / 32) * sn_host[z]);
+        a.z[j - i] = z;
+        a.nn[j - i] = sn_host[z];
+        a.plan[j - i] = (int)(table.size() / 32);  // 128-B NccMRec records
+        for (int k = 0; k < sn_host[z]; k++) a.view[j - i][k] = views[j][k];
+        table.insert(table.end(), mplan[j].table.begin(), mplan[j].table.end());
+        j++;
+      }
+      a.nref = j - i;
+      int rc = 0;
+      const int32_t* dev = plan_upload(ctx, table, &rc);
+      if (rc) return rc;
+      const WtaOut wo{levels_dev, disp + P * i, conf ? conf + P * i : nullptr};
+      rc = launch_ncc_mfma(ctx, stats, pk, dev, a, wo, bw, tmax);
+      if (rc) return rc;
+      i = j;
+      continue;
+    }
     int bwt = ch[i].bwt, pkp = ch[i].plan.pk_pairs, stp = ch[i].plan.st_pairs;
     int par = ch[i].plan.par();
     size_t cap = ch[i].cap;
     int j = i + 1;
-    while (!vol && j < n && j - i < maxrun && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw && ch[j].nb == ch[i].nb) {
+    while (!vol && j < n && !mf[j] && j - i < maxrun && ch[j].dpw == ch[i].dpw && ch[j].nw == ch[i].nw &&
+           ch[j].nb == ch[i].nb) {
       const int b2 = std::max(bwt, ch[j].bwt);
       const int p2 = std::max(pkp, ch[j].plan.pk_pairs), s2 = std::max(stp, ch[j].plan.st_pairs);
       const size_t c2 = std::min(cap, ch[j].cap);

@@ -1,0 +1,402 @@
+// Matrix-core form of the fused NCC sweep + WTA (K = 5, horizontal
+// neighbours): the definition and the outputs are ncc.hip's (k_ncc_volume
+// with FUSE), bit for bit; launch_ncc_refs (ncc.hip) picks it per reference
+// view.  See the comment at NccMRec for the formulation.
+#include <algorithm>
+#include <type_traits>
+
+#include "ncc_common.h"
+
+namespace mvs {
+namespace ncc {
+namespace {
+
+// ---- matrix-core form of the fused sweep (K = 5, horizontal neighbours) ----
+//
+// The correlation Srp'(x, y, d) = sum_{j, i} r'(x+i, y+j) p'(x+i-tx(d), y+j)
+// as a GEMM whose output lands in the SAME (pixel, level) layout for every
+// neighbour, so the neighbour maximum stays in registers:
+//   C[m][n] = sum_k A[m][k] B[k][n],   m = (xx, yy) of a 4 x 4 pixel block,
+//   n = level d0 + n of a 16-level block, k = (row, column) of the block's
+//   8 x 8 window footprint (rows y0b-2 .. y0b+5, columns x0b-2 .. x0b+5);
+//   A[m][k] = r'(column, row) where the tap lies in pixel m's 5 x 5 window, else 0
+//             (the REFERENCE, banded: built once per tile, reused for every
+//             neighbour and level);
+//   B[k][n] = p'(column - tx(d0+n), row)   (the neighbour: its row-pair pk entry
+//             at column x0b - tx, i.e. one aligned 16-byte LDS read per lane).
+// k = 64 = 4 row pairs x 16 bytes is exactly one v_mfma_i32_16x16x64_i8 and
+// exactly the pk plane's row-pair entry, so a lane's B operand for row pair g
+// is ONE ds_read_b128 from the band the LDS-DMA stages anyway.  The MFMA's
+// accumulator starts at the bits of 1.5 * 2^23: read as a float the result is
+// 1.5 * 2^23 + Srp' exactly (|Srp'| < 2^22), one v_pk_add_f32 per 2 cells.
+// Per lane the output is C[4 (l >> 4) + r][l & 15]: pixel column xx = l >> 4,
+// rows yy = r = 0..3, level l & 15 -- a fixed pixel column and level per lane,
+// so the neighbour stats (a, b of rows y0b..y0b+3 at column x - tx) are two
+// ds_read_b128 per lane, and the finish x = fma(-Sr', b, Srp' a) and the
+// maximum are the scalar kernel's operations in the same order (bit-identical).
+// Per wave and neighbour step: 4 pixel blocks (8 columns x 8 rows) x 2 level
+// blocks = 8 MFMAs for 2,048 view-cells, against 192 dot4 of the scalar form.
+// Lane l holds the levels of class l & 15 (16 apart): the fold keeps the same
+// (smallest, its level, second smallest) triple per cell, and the 16 classes
+// of a pixel are merged through LDS as the scalar kernel merges its waves.
+struct alignas(128) NccMRec {
+  int txmax, tymax;  // band origin, as NccRec (tymax = 0: every shift horizontal)
+  int bhp, shp;      // pk / stats pair rows to stage | (column span) << 16, as NccRec
+  int colo[16];      // 32 x int16: per level j of the chunk, txmax - tx(j) (band column of reference column x0)
+  int pad[12];
+};
+static_assert(sizeof(NccMRec) == 128, "one 128-B record per (chunk, neighbour)");
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int kMfMergeStride = 257;  // LDS merge rows: 256 pixels + 1 (16 classes on distinct banks)
+
+template <int BW>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_mfma(
+    const uint2* __restrict__ stats, const uint2* __restrict__ pk, const NccMRec* __restrict__ plan, NccArgs a,
+    WtaOut wo) {
+  constexpr int R = 2, TH = 8, NW = 8, DC = 32, NK = 25, NR = TH + 2 * R;
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int nbuf = (a.pk_pairs + a.st_pairs) * BW;  // uint4 per neighbour buffer
+  u32x4* nbase = (u32x4*)smem;                      // 2 x {npk[pk_pairs][BW], nst[st_pairs][BW]}
+  const int band_bytes = max(2 * nbuf * 16, 3 * 16 * kMfMergeStride * 4);
+  float* rsn_l = (float*)(smem + band_bytes);  // [64][TH] -Sr' of the tile's pixels (column-major)
+  float* srl = rsn_l + 64 * TH;                 // [64][TH] s_r
+  short* colo_l = (short*)(srl + 64 * TH);      // [T][32] band column offsets per step and level
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int W = a.W, H = a.H;
+  const int Hp2 = (H + 1) >> 1;
+  const long Pv = (long)W * Hp2 * 2;
+  const long P = (long)W * H;
+  const int bid = blockIdx.x, grp = bid & 7;  // XCD-aware tile map, as k_ncc_volume
+  const int tg = grp * a.tiles_per_xcd + (bid >> 3);
+  if (tg >= a.ntiles * a.nref) return;
+  const int ref = tg / a.ntiles, tile = tg - ref * a.ntiles;
+  const int x0 = (tile % a.tiles_x) * 64;
+  const int y0 = (tile / a.tiles_x) * TH;  // even
+  const int nn = a.nn[ref], T = a.nch * nn;
+  const NccMRec* rec = plan + a.plan[ref];
+
+  // LDS-DMA staging of step t's bands (k_ncc_volume's stage, one record per step)
+  auto stage = [&](int t, int n, int b) {
+    const NccMRec& e = rec[t];
+    const int bhp = e.bhp, shp = e.shp & 0xffff, span = e.shp >> 16, nblk = (span + 127) >> 6;
+    const int pm0 = (y0 - R - e.tymax) >> 1, sm0 = (y0 - e.tymax) >> 1;
+    const long vo = (long)a.view[ref][n] * Pv;
+    u32x4* npk = nbase + b * nbuf;
+    u32x4* nst = npk + a.pk_pairs * BW;
+    for (int cb = 0; cb < nblk; cb++) {
+      const int c0 = min(cb * 64, span);
+      const int xx = min(max(x0 - e.txmax + c0 + lane, 0), W - 1);
+      const uint2* gpk = pk + vo + 2 * xx;
+      const uint2* gst = stats + vo + 2 * xx;
+      for (int i = wave; i < bhp; i += NW) glds_b128(gpk + 2L * W * min(max(pm0 + i, 0), Hp2 - 1), npk + i * BW + c0);
+      for (int i = wave; i < shp; i += NW) glds_b128(gst + 2L * W * min(max(sm0 + i, 0), Hp2 - 1), nst + i * BW + c0);
+    }
+  };
+
+  // the steps' level -> band column offsets, into LDS (before the pipeline)
+  for (int i = tid; i < T * 16; i += NW * 64) ((int*)colo_l)[i] = rec[i >> 4].colo[i & 15];
+  stage(0, 0, 0);
+  const long zo = (long)a.z[ref] * Pv;
+  // wave 0: -Sr' and s_r of the tile's 64 x TH pixels (lane = column), as k_ncc_volume
+  if (wave == 0) {
+    const int x = x0 + lane, xc = min(x, W - 1);
+    int rsum[NR], rsq[NR];
+#pragma unroll
+    for (int k = 0; k < NR; k++) {
+      const uint2 v = pk[zo + pair_index(min(max(y0 - R + k, 0), H - 1), xc, W)];
+      const unsigned lo = v.x, hi = v.y & 0xffu;
+      rsum[k] = dot4(lo, 0x01010101u, dot4(hi, 0x01010101u, 0));
+      rsq[k] = dot4(lo, lo, dot4(hi, hi, 0));
+    }
+    float nsr[TH], sr[TH];
+#pragma unroll
+    for (int o = 0; o < TH; o++) {
+      int s1 = 0, s2 = 0;
+#pragma unroll
+      for (int k = 0; k < 2 * R + 1; k++) {
+        s1 += rsum[o + k];
+        s2 += rsq[o + k];
+      }
+      const int y = y0 + o;
+      const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
+      const int var = NK * s2 - s1 * s1;
+      sr[o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
+      nsr[o] = -(float)s1;
+    }
+#pragma unroll
+    for (int o = 0; o < TH; o += 4) {
+      *(f32x4*)(rsn_l + lane * TH + o) = f32x4{nsr[o], nsr[o + 1], nsr[o + 2], nsr[o + 3]};
+      *(f32x4*)(srl + lane * TH + o) = f32x4{sr[o], sr[o + 1], sr[o + 2], sr[o + 3]};
+    }
+  }
+  // the reference operands: pixel block (xb, yb) of this wave = columns
+  // x0 + 8 wave + 4 xb .. +3, rows y0 + 4 yb .. +3.  Lane l supplies row
+  // m = l & 15 (pixel xx = m >> 2, yy = m & 3) and row pair g = l >> 4 of the
+  // footprint: the 16-byte pk entry at column x0b, masked to the pixel's window
+  // (bytes xx .. xx+4 of a row; footprint rows yy .. yy+4)
+  i32x4 A[2][2];
+  {
+    const int mA = lane & 15, xxA = mA >> 2, yyA = mA & 3, g = lane >> 4;
+    unsigned msk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int h = k >> 1, rr = 2 * g + h;
+      unsigned mk = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int t = 4 * (k & 1) + b;
+        if (t >= xxA && t <= xxA + 4 && rr >= yyA && rr <= yyA + 4) mk |= 0xffu << (8 * b);
+      }
+      msk[k] = mk;
+    }
+#pragma unroll
+    for (int xb = 0; xb < 2; xb++)
+#pragma unroll
+      for (int yb = 0; yb < 2; yb++) {
+        const int xcol = min(x0 + 8 * wave + 4 * xb, W - 1);
+        const int pr = min(max((y0 >> 1) - 1 + 2 * yb + g, 0), Hp2 - 1);
+        const u32x4 v = *(const u32x4*)(pk + zo + (((long)pr * W + xcol) << 1));
+        A[xb][yb] = i32x4{(int)(v.x & msk[0]), (int)(v.y & msk[1]), (int)(v.z & msk[2]), (int)(v.w & msk[3])};
+      }
+  }
+  __syncthreads();
+
+  float E[2][2][2][4];  // [xb][yb][level block][row]: max over the neighbours so far
+  float wv0[2][2][4], wv1[2][2][4];
+  unsigned wi0p[2][2][2];  // level of the smallest, rows (2p, 2p+1) as the halves of one register (0xffff: none)
+#pragma unroll
+  for (int xb = 0; xb < 2; xb++)
+#pragma unroll
+    for (int yb = 0; yb < 2; yb++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        wv0[xb][yb][r] = kWtaInit;
+        wv1[xb][yb][r] = kWtaInit;
+      }
+      wi0p[xb][yb][0] = wi0p[xb][yb][1] = 0xffffffffu;
+    }
+  const i32x4 bias = i32x4{kMagicI, kMagicI, kMagicI, kMagicI};
+
+  // fold chunk c's levels into the per-cell triples (k_ncc_volume's fold; this
+  // lane's levels are c * 32 + 16 db + (l & 15), in increasing order)
+  auto fold = [&](int c) {
+    const int ln = lane_now();
+    const bool tail = (c + 1) * DC > a.D;
+#pragma unroll
+    for (int xb = 0; xb < 2; xb++)
+#pragma unroll
+      for (int yb = 0; yb < 2; yb++) {
+        const f32x4 sq = *(const f32x4*)(srl + (8 * wave + 4 * xb + (ln >> 4)) * TH + 4 * yb);
+#pragma unroll
+        for (int db = 0; db < 2; db++) {
+          const int dl = c * DC + 16 * db + (ln & 15);
+          const unsigned dl2 = (unsigned)dl * 0x10001u;
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 e = f32x2{E[xb][yb][db][r], E[xb][yb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
+            f32x2 cst = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
+            if (tail && dl >= a.D) cst = f32x2{INFINITY, INFINITY};  // dummy level past the end
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              const float cc = cst[h];
+              const unsigned hm = h ? 0xffff0000u : 0x0000ffffu;
+              unsigned& wp = wi0p[xb][yb][r >> 1];
+              wv1[xb][yb][r + h] = vmed3(wv0[xb][yb][r + h], wv1[xb][yb][r + h], cc);
+              wp = cc < wv0[xb][yb][r + h] ? (wp & ~hm) | (dl2 & hm) : wp;
+              wv0[xb][yb][r + h] = vmin(wv0[xb][yb][r + h], cc);
+            }
+          }
+        }
+      }
+  };
+
+  // one pipeline step t = c * nn + n (chunks outer, neighbours inner; the
+  // chunk's first neighbour assigns E, as k_ncc_volume's PEEL)
+  auto step = [&](int t, int n, int cprev, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
+    const int n1 = n + 1 == nn ? 0 : n + 1;
+    // A block's B entry sits at column x0b - tx, up to 3 columns left of its
+    // cells' neighbour pixels: a valid cell (neighbour column 2, xx = 3) reads
+    // the entry of image column -1, which the clamped DMA filled with column
+    // 0's.  Where the band holds column -1 (tiles at the left image edge),
+    // that entry becomes the pk plane's definition: column 0's bytes one place
+    // later (its bytes 0..2 lie outside the image and meet masked taps only).
+    {
+      const int jf = rec[t].txmax - x0 - 1;  // band column of image column -1 (scalar)
+      if (jf >= 0 && jf + 1 < 64 + (rec[t].shp >> 16)) {  // inside the band's 64 + span columns
+        if (tid < a.pk_pairs) {
+          u32x4* e = nbase + (t & 1) * nbuf + tid * BW + jf;
+          const u32x4 v = e[1];
+          *e = u32x4{v.x << 8, (v.y << 8) | (v.x >> 24), v.z << 8, (v.w << 8) | (v.z >> 24)};
+        }
+        __syncthreads();
+      }
+    }
+    if (t + 1 < T) stage(t + 1, n1, (t + 1) & 1);
+    if (FIRST && cprev >= 0) fold(cprev);
+    const u32x4* npk = nbase + (t & 1) * nbuf;
+    const u32x4* nst = npk + a.pk_pairs * BW;
+    const int ln = lane_now();
+    const int g = ln >> 4;
+    int cl[2];
+#pragma unroll
+    for (int db = 0; db < 2; db++) cl[db] = colo_l[t * DC + 16 * db + (ln & 15)];
+#pragma unroll
+    for (int xb = 0; xb < 2; xb++)
+#pragma unroll
+      for (int yb = 0; yb < 2; yb++) {
+        const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
+#pragma unroll
+        for (int db = 0; db < 2; db++) {
+          const int colB = 8 * wave + 4 * xb + cl[db];  // pk band column of the block's first pixel column
+          const u32x4 bv = npk[(2 * yb + g) * BW + colB];
+          const i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, bv), bias, 0, 0, 0);
+          const f32x4 s0 = __builtin_bit_cast(f32x4, nst[(2 * yb) * BW + colB + g]);      // rows 0, 1
+          const f32x4 s1 = __builtin_bit_cast(f32x4, nst[(2 * yb + 1) * BW + colB + g]);  // rows 2, 3
+#pragma unroll
+          for (int p = 0; p < 2; p++) {
+            const f32x4 sv = p ? s1 : s0;
+            const f32x2 f = f32x2{__int_as_float(acc[2 * p]), __int_as_float(acc[2 * p + 1])} - f32x2{kMagicF, kMagicF};
+            const f32x2 xv = __builtin_elementwise_fma(f32x2{nsr[2 * p], nsr[2 * p + 1]}, f32x2{sv.z, sv.w},
+                                                       f * f32x2{sv.x, sv.y});
+            if (FIRST) {
+              E[xb][yb][db][2 * p] = xv.x;
+              E[xb][yb][db][2 * p + 1] = xv.y;
+            } else {
+              E[xb][yb][db][2 * p] = vmax(E[xb][yb][db][2 * p], xv.x);
+              E[xb][yb][db][2 * p + 1] = vmax(E[xb][yb][db][2 * p + 1], xv.y);
+            }
+          }
+        }
+      }
+    __syncthreads();  // step t+1's bands landed; this buffer free for t+2
+  };
+  {
+    int t = 0;
+    for (int c = 0; c < a.nch; c++) {
+      step(t++, 0, c - 1, std::true_type{});
+      for (int n = 1; n < nn; n++) step(t++, n, -1, std::false_type{});
+    }
+  }
+  fold(a.nch - 1);
+
+  // merge the 16 level classes of every pixel through LDS (the band buffers
+  // are free: every wave passed the loop's last barrier), one half tile of
+  // 64 x 4 pixels at a time; one thread per pixel, k_ncc_volume's merge
+  float* m0 = (float*)smem;
+  float* m1 = m0 + 16 * kMfMergeStride;
+  int* mi = (int*)(m1 + 16 * kMfMergeStride);
+#pragma unroll
+  for (int yb = 0; yb < 2; yb++) {
+    {
+      const int ln = lane_now(), cls = ln & 15;
+#pragma unroll
+      for (int xb = 0; xb < 2; xb++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int q = cls * kMfMergeStride + r * 64 + 8 * wave + 4 * xb + (ln >> 4);
+          const unsigned v = (r & 1) ? wi0p[xb][yb][r >> 1] >> 16 : wi0p[xb][yb][r >> 1] & 0xffffu;
+          m0[q] = wv0[xb][yb][r];
+          m1[q] = wv1[xb][yb][r];
+          mi[q] = v == 0xffffu ? -1 : (int)v;
+        }
+    }
+    __syncthreads();
+    if (tid < 256) {
+      const int q = tid, xx = x0 + (q & 63), yy = y0 + 4 * yb + (q >> 6);
+      float bv = m0[q];
+      int bi = mi[q];
+#pragma unroll
+      for (int w = 1; w < 16; w++) {
+        const float v = m0[w * kMfMergeStride + q];
+        const int i = mi[w * kMfMergeStride + q];
+        if (v < bv || (v == bv && i >= 0 && i < bi)) {
+          bv = v;
+          bi = i;
+        }
+      }
+      float c2 = kWtaInit;
+#pragma unroll
+      for (int w = 0; w < 16; w++) {
+        const int i = mi[w * kMfMergeStride + q];
+        const float v = (i >= bi - 1 && i <= bi + 1) ? m1[w * kMfMergeStride + q] : m0[w * kMfMergeStride + q];
+        c2 = vmin(c2, v);
+      }
+      if (xx < W && yy < H) {
+        const long p = P * ref + (long)yy * W + xx;
+        wo.disp[p] = bi >= 0 ? wo.levels[bi] : 0.0f;
+        if (wo.conf) wo.conf[p] = (bi < 0 || c2 == kWtaInit) ? 0.0f : c2 - bv;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+
+template <int BW>
+int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec* plan, NccArgs& a,
+                   const WtaOut& wo, int tmax) {
+  const int variant[8] = {5, 8, 16, 8, BW, kParEven, 1, 2};
+  std::copy(variant, variant + 8, ctx->ncc_last);
+  a.tiles_x = (a.W + 63) / 64;
+  a.ntiles = a.tiles_x * ((a.H + 7) / 8);
+  a.tiles_per_xcd = (a.nref * a.ntiles + 7) / 8;
+  a.nch = (a.D + 31) / 32;
+  const size_t lds = std::max((size_t)2 * 16 * (a.pk_pairs + a.st_pairs) * BW, (size_t)3 * 16 * kMfMergeStride * 4) +
+                     2 * 64 * 8 * 4 + (size_t)tmax * 32 * 2;
+  auto kern = k_ncc_mfma<BW>;
+  if (lds > 64 * 1024)
+    MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            "hipFuncSetAttribute(ncc mfma lds)");
+  hipLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(512), lds, ctx->stream, stats, pk, plan, a, wo);
+  MVS_LAUNCH_CHECK("k_ncc_mfma (fused WTA)");
+  return 0;
+}
+
+}  // namespace
+
+// the matrix-core form's plan: one NccMRec per (32-level chunk, neighbour)
+NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx) {
+  constexpr int DC = 32, RW = sizeof(NccMRec) / 4;
+  const int nch = (D + DC - 1) / DC;
+  NccPlanM p;
+  p.table.assign((size_t)nch * nn * RW, 0);
+  int spx = 0;
+  auto tx_of = [&](int dl, int n) { return (int)roundf(levels[dl] * fdx[n]); };
+  for (int c = 0; c < nch; c++)
+    for (int n = 0; n < nn; n++) {
+      int txmin = 1 << 30, txmax = -(1 << 30);
+      for (int dl = c * DC; dl < std::min(D, c * DC + DC); dl++) {
+        txmin = std::min(txmin, tx_of(dl, n));
+        txmax = std::max(txmax, tx_of(dl, n));
+      }
+      int32_t* e = p.table.data() + ((size_t)c * nn + n) * RW;
+      e[0] = txmax;
+      e[1] = 0;
+      e[2] = 6;                          // pk pair rows: y0-2 .. y0+9 (K = 5, TH = 8, no vertical shift)
+      e[3] = 4 | ((txmax - txmin) << 16);  // stats pair rows y0 .. y0+7 | the chunk's column span
+      int16_t* co = (int16_t*)(e + 4);
+      for (int j = 0; j < DC; j++) {
+        const int dl = c * DC + j;
+        co[j] = (int16_t)(dl < D ? txmax - tx_of(dl, n) : 0);  // dummy level past the end: in-band
+      }
+      spx = std::max(spx, txmax - txmin);
+    }
+  p.band_w = 64 + spx;
+  return p;
+}
+
+
+int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
+                    const WtaOut& wo, int bw, int tmax) {
+  const NccMRec* pl = (const NccMRec*)plan_dev;
+  return bw <= 64    ? launch_mfma_bw<64>(ctx, stats, pk, pl, a, wo, tmax)
+         : bw <= 80  ? launch_mfma_bw<80>(ctx, stats, pk, pl, a, wo, tmax)
+         : bw <= 96  ? launch_mfma_bw<96>(ctx, stats, pk, pl, a, wo, tmax)
+         : bw <= 128 ? launch_mfma_bw<128>(ctx, stats, pk, pl, a, wo, tmax)
+                     : launch_mfma_bw<192>(ctx, stats, pk, pl, a, wo, tmax);
+}
+
+}  // namespace ncc
+}  // namespace mvs

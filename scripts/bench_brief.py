@@ -12,7 +12,7 @@ if "roofline" in j:
     out["roofline"] = j["roofline"]["frac"]
 rs = j.get("roofline_sweep") or {}
 out["fused_ms_view"] = rs.get("avg_ms_per_view")
-for k in ("reference_cost", "reference_defaults", "two_pass_variant", "view_sharded"):
+for k in ("reference_cost", "reference_defaults", "c3", "two_pass_variant", "view_sharded"):
     if isinstance(j.get(k), dict):
         v = j[k]
         out[k] = v.get("error") or (v.get("value"), v.get("ms_per_step"),

@@ -43,7 +43,7 @@ for s in "$@"; do
         for side in A B; do
           if [ $side = A ]; then export MVS_LIB=$PWD/ab/libmvs_A.so; else unset MVS_LIB; fi
           timeout -k 10 300 python3 bench.py --config $C --no-cpu-baseline --no-sharded --no-reference-cost \
-            --no-reference-defaults ${ABARGS:-} > $O/ab_$side.json 2> $O/ab_$side.err || fail "$s $side" $O/ab_$side.err
+            --no-reference-defaults --no-c3 ${ABARGS:-} > $O/ab_$side.json 2> $O/ab_$side.err || fail "$s $side" $O/ab_$side.err
           python3 -c "import json;j=json.load(open('$O/ab_$side.json'));print('$C $side', j['ms_per_step'], j['value'])" \
             | tee -a $O/ab_$C.txt
         done
@@ -55,7 +55,7 @@ for s in "$@"; do
         for side in A B; do
           if [ $side = A ]; then unset $VAR; else export "$KV"; fi
           timeout -k 10 300 python3 bench.py --config $C --no-cpu-baseline --no-sharded --no-reference-cost \
-            --no-reference-defaults ${ABARGS:-} > $O/abenv_$side.json 2> $O/abenv_$side.err || fail "$s $side" $O/abenv_$side.err
+            --no-reference-defaults --no-c3 ${ABARGS:-} > $O/abenv_$side.json 2> $O/abenv_$side.err || fail "$s $side" $O/abenv_$side.err
           python3 -c "import json;j=json.load(open('$O/abenv_$side.json'));print('$C $KV $side', j['ms_per_step'], j['value'], (j.get('roofline_sweep') or {}).get('avg_ms_per_view'))" \
             | tee -a $O/abenv_$C.txt
         done
@@ -64,7 +64,7 @@ for s in "$@"; do
     trace:*)
       C=${s#trace:}
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_$C -o run -- python3 bench.py --config $C \
-        --steps 5 --warmup 2 --no-cpu-baseline --no-sharded --no-reference-cost --no-reference-defaults \
+        --steps 5 --warmup 2 --no-cpu-baseline --no-sharded --no-reference-cost --no-reference-defaults --no-c3 \
         > $O/trace_$C.json 2> $O/trace_$C.err || fail "$s" $O/trace_$C.err
       python3 scripts/kstats.py $O/trace_$C > $O/trace_$C.txt 2>&1; head -12 $O/trace_$C.txt ;;
     pmc:*)

@@ -30,8 +30,30 @@ def db(path):
 
 
 def short(name):
-    n = name.replace("mvs::(anonymous namespace)::", "").replace("void ", "")
+    n = name.replace("mvs::ncc::(anonymous namespace)::", "").replace("mvs::(anonymous namespace)::", "")
+    n = n.replace("void ", "")
     return n.split("(")[0].strip()
+
+
+NCC_SOURCES = ("cl_multiview_stereo_amd/csrc/ncc.hip", "cl_multiview_stereo_amd/csrc/ncc_mfma.hip",
+               "cl_multiview_stereo_amd/csrc/ncc_common.h")
+
+
+def ncc_src_sha16(root=ROOT):
+    """sha256 (16 hex digits) of the NCC sweep sources: bench.py compares it with
+    the tree it runs from and marks a PMC-derived fraction stale on a mismatch."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in NCC_SOURCES:
+        p = os.path.join(root, f)
+        if os.path.exists(p):
+            h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def fused_kernel(name):
+    """The fused sweep + WTA kernels: k_ncc_volume<..., true, NB> and k_ncc_mfma<BW>."""
+    return name.startswith("k_ncc_mfma") or (name.startswith("k_ncc_volume") and ", true" in name)
 
 
 def main():
@@ -54,7 +76,7 @@ def main():
             w.writerow([short(r[0]), r[1], round(r[2], 1), round(r[3], 1), round(r[4], 3)])
     pmc = defaultdict(dict)
     for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write"), ("SQ_INSTS_VALU", "pmc_valu"),
-                         ("SQ_INSTS_LDS", "pmc_valu")):
+                         ("SQ_INSTS_LDS", "pmc_valu"), ("SQ_INSTS_MFMA", "pmc_valu")):
         d = db(os.path.join(src, sub))
         if d is None:
             continue
@@ -79,7 +101,7 @@ def main():
                    "hbm_bytes_per_launch": pmc[wta]["hbm_bytes_per_launch"],
                    "note": "2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes", "config": cfg, **shape},
                   open(os.path.join(out, f"pmc_wta_{cfg}.json"), "w"), indent=1)
-    ncc = [k for k in sorted(pmc) if k.startswith("k_ncc_volume") and "SQ_INSTS_VALU_per_launch" in pmc[k]]
+    ncc = [k for k in sorted(pmc) if k.startswith(("k_ncc_volume", "k_ncc_mfma")) and "SQ_INSTS_VALU_per_launch" in pmc[k]]
     if ncc:
         extra = {}
         # the fused sweep runs several reference views per launch
@@ -87,23 +109,26 @@ def main():
         # views that pass's bench process swept (bench.py profile_counts)
         try:
             counts = json.load(open(os.path.join(src, "pmc_valu_bench.json")))["profile_counts"]
-            tot = sum(pmc[k]["SQ_INSTS_VALU_per_launch"] * pmc[k]["launches"] for k in ncc if ", true" in k)
+            tot = sum(pmc[k]["SQ_INSTS_VALU_per_launch"] * pmc[k]["launches"] for k in ncc if fused_kernel(k))
+            mf = sum(pmc[k].get("SQ_INSTS_MFMA_per_launch", 0.0) * pmc[k]["launches"] for k in ncc if fused_kernel(k))
             if counts.get("ncc_wta_views") and tot:
                 extra = {"fused_valu_wave_insts_per_view": tot / counts["ncc_wta_views"],
                          "fused_views_in_pass": counts["ncc_wta_views"],
-                         "fused_launches_in_pass": sum(pmc[k]["launches"] for k in ncc if ", true" in k)}
+                         "fused_launches_in_pass": sum(pmc[k]["launches"] for k in ncc if fused_kernel(k))}
+                if mf:
+                    extra["fused_mfma_insts_per_view"] = mf / counts["ncc_wta_views"]
         except (OSError, ValueError, KeyError):
             pass
         json.dump({k: {"valu_wave_insts_per_launch": pmc[k]["SQ_INSTS_VALU_per_launch"],
                        "lds_wave_insts_per_launch": pmc[k].get("SQ_INSTS_LDS_per_launch"),
                        "launches": pmc[k]["launches"]} for k in ncc} | extra |
                   {"source": f"profiles/{tag}_pmc.json", "note": "SQ_INSTS_VALU / SQ_INSTS_LDS, own --pmc pass",
-                   "config": cfg, **shape},
+                   "config": cfg, "ncc_src_sha16": ncc_src_sha16(), **shape},
                   open(os.path.join(out, f"pmc_ncc_{cfg}.json"), "w"), indent=1)
     for r in rows[:8]:
         print(f"{short(r[0]):40s} calls={r[1]:5d} avg={r[3]:9.3f} us  {r[4]:6.2f}%")
     for k in sorted(pmc):
-        if k.split("<")[0] in ("k_wta", "k_ncc_volume", "k_cvt", "k_update_tiles", "k_assign", "k_box_stats"):
+        if k.split("<")[0] in ("k_wta", "k_ncc_volume", "k_ncc_mfma", "k_cvt", "k_update_tiles", "k_assign", "k_box_stats"):
             print(k, {a: round(b / 1e6, 2) for a, b in pmc[k].items() if "bytes" in a})
 
 

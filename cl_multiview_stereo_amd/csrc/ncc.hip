@@ -791,7 +791,7 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
       if (fdy[k] != 0.0f) horiz = false;
     }
     if (mf_on && horiz && nn > 0) {
-      mplan[r] = make_plan_mfma(levels_host, D, nn, fdx);
+      mplan[r] = make_plan_mfma(levels_host, D, nn, fdx, mfma_tile_rows());
       if (mplan[r].band_w <= 192) {
         mf[r] = 1;
         continue;
@@ -815,8 +815,8 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
       a.W = W;
       a.H = H;
       a.D = D;
-      a.pk_pairs = 6;
-      a.st_pairs = 4;
+      a.pk_pairs = (mfma_tile_rows() + 4) / 2;
+      a.st_pairs = mfma_tile_rows() / 2;
       std::vector<int32_t> table;
       while (j < n && mf[j] && j - i < maxrun) {
         const int z = z0 + j;

@@ -167,7 +167,8 @@ struct NccPlanM {
   std::vector<int32_t> table;
   int band_w = 0;  // columns per band pair row: 64 + the widest chunk span
 };
-NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx);
+NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, int TH);
+int mfma_tile_rows();  // 8 (default) or 4 (MVS_NCC_MFMA_TH=4)
 int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
                     const WtaOut& wo, int bw, int tmax);
 

@@ -3,6 +3,7 @@
 // with FUSE), bit for bit; launch_ncc_refs (ncc.hip) picks it per reference
 // view.  See the comment at NccMRec for the formulation.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ncc_common.h"
@@ -49,13 +50,20 @@ static_assert(sizeof(NccMRec) == 128, "one 128-B record per (chunk, neighbour)")
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int kMfMergeStride = 257;  // LDS merge rows: 256 pixels + 1 (16 classes on distinct banks)
 
-template <int BW>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_mfma(
+// TH: tile rows (4: a wave owns 8 columns x 4 rows = 2 pixel blocks; 8: 8 x 8 =
+// 4 blocks, twice the per-lane state).  TAIL: D % 32 != 0, the last chunk
+// carries dummy levels past the end.
+template <int BW, int TH, bool TAIL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5 : 4))) void k_ncc_mfma(
     const uint2* __restrict__ stats, const uint2* __restrict__ pk, const NccMRec* __restrict__ plan, NccArgs a,
     WtaOut wo) {
-  constexpr int R = 2, TH = 8, NW = 8, DC = 32, NK = 25, NR = TH + 2 * R;
+  constexpr int R = 2, NW = 8, DC = 32, NK = 25, NR = TH + 2 * R, NYB = TH / 4;  // NYB: pixel-block rows
+  // band row pitch: BW + 1 columns of 16 B, so a lane group's B reads in two
+  // rows (row pairs g, g + 1) fall on different banks when the shift per level
+  // is even (|dx| = 2: conflict-free instead of 2-way)
+  constexpr int BWP = BW + 1;
   extern __shared__ __align__(16) uint8_t smem[];
-  const int nbuf = (a.pk_pairs + a.st_pairs) * BW;  // uint4 per neighbour buffer
+  const int nbuf = (a.pk_pairs + a.st_pairs) * BWP;  // uint4 per neighbour buffer
   u32x4* nbase = (u32x4*)smem;                      // 2 x {npk[pk_pairs][BW], nst[st_pairs][BW]}
   const int band_bytes = max(2 * nbuf * 16, 3 * 16 * kMfMergeStride * 4);
   float* rsn_l = (float*)(smem + band_bytes);  // [64][TH] -Sr' of the tile's pixels (column-major)
@@ -76,21 +84,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   const int nn = a.nn[ref], T = a.nch * nn;
   const NccMRec* rec = plan + a.plan[ref];
 
-  // LDS-DMA staging of step t's bands (k_ncc_volume's stage, one record per step)
+  // LDS-DMA staging of step t's bands (k_ncc_volume's stage, one record per
+  // step).  Every shift is horizontal, so a step's band rows are the same
+  // image rows for every step: wave w stages pk pair row w (w < bhp) and stats
+  // pair row w (w < shp), whose clamped row offsets are computed once per tile
+  const int bhp = (TH + 4) / 2, shp = TH / 2;
+  const long pk_row = 2L * W * min(max((y0 - R) / 2 + wave, 0), Hp2 - 1);  // (y0 - R) even: y0 even, R = 2
+  const long st_row = 2L * W * min(max(y0 / 2 + wave, 0), Hp2 - 1);
   auto stage = [&](int t, int n, int b) {
     const NccMRec& e = rec[t];
-    const int bhp = e.bhp, shp = e.shp & 0xffff, span = e.shp >> 16, nblk = (span + 127) >> 6;
-    const int pm0 = (y0 - R - e.tymax) >> 1, sm0 = (y0 - e.tymax) >> 1;
+    const int span = e.shp >> 16, nblk = (span + 127) >> 6;
     const long vo = (long)a.view[ref][n] * Pv;
     u32x4* npk = nbase + b * nbuf;
-    u32x4* nst = npk + a.pk_pairs * BW;
+    u32x4* nst = npk + a.pk_pairs * BWP;
+    const int xb0 = x0 - e.txmax + lane;
     for (int cb = 0; cb < nblk; cb++) {
       const int c0 = min(cb * 64, span);
-      const int xx = min(max(x0 - e.txmax + c0 + lane, 0), W - 1);
-      const uint2* gpk = pk + vo + 2 * xx;
-      const uint2* gst = stats + vo + 2 * xx;
-      for (int i = wave; i < bhp; i += NW) glds_b128(gpk + 2L * W * min(max(pm0 + i, 0), Hp2 - 1), npk + i * BW + c0);
-      for (int i = wave; i < shp; i += NW) glds_b128(gst + 2L * W * min(max(sm0 + i, 0), Hp2 - 1), nst + i * BW + c0);
+      const int xx = min(max(xb0 + c0, 0), W - 1);
+      if (wave < bhp) glds_b128(pk + vo + pk_row + 2 * xx, npk + wave * BWP + c0);
+      if (wave < shp) glds_b128(stats + vo + st_row + 2 * xx, nst + wave * BWP + c0);
     }
   };
 
@@ -135,7 +147,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   // m = l & 15 (pixel xx = m >> 2, yy = m & 3) and row pair g = l >> 4 of the
   // footprint: the 16-byte pk entry at column x0b, masked to the pixel's window
   // (bytes xx .. xx+4 of a row; footprint rows yy .. yy+4)
-  i32x4 A[2][2];
+  i32x4 A[2][NYB];
   {
     const int mA = lane & 15, xxA = mA >> 2, yyA = mA & 3, g = lane >> 4;
     unsigned msk[4];
@@ -153,7 +165,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
     for (int xb = 0; xb < 2; xb++)
 #pragma unroll
-      for (int yb = 0; yb < 2; yb++) {
+      for (int yb = 0; yb < NYB; yb++) {
         const int xcol = min(x0 + 8 * wave + 4 * xb, W - 1);
         const int pr = min(max((y0 >> 1) - 1 + 2 * yb + g, 0), Hp2 - 1);
         const u32x4 v = *(const u32x4*)(pk + zo + (((long)pr * W + xcol) << 1));
@@ -162,13 +174,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   }
   __syncthreads();
 
-  float E[2][2][2][4];  // [xb][yb][level block][row]: max over the neighbours so far
-  float wv0[2][2][4], wv1[2][2][4];
-  unsigned wi0p[2][2][2];  // level of the smallest, rows (2p, 2p+1) as the halves of one register (0xffff: none)
+  float E[2][NYB][2][4];  // [xb][yb][level block][row]: max over the neighbours so far
+  float wv0[2][NYB][4], wv1[2][NYB][4];
+  unsigned wi0p[2][NYB][2];  // level of the smallest, rows (2p, 2p+1) as the halves of one register (0xffff: none)
 #pragma unroll
   for (int xb = 0; xb < 2; xb++)
 #pragma unroll
-    for (int yb = 0; yb < 2; yb++) {
+    for (int yb = 0; yb < NYB; yb++) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         wv0[xb][yb][r] = kWtaInit;
@@ -182,11 +194,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   // lane's levels are c * 32 + 16 db + (l & 15), in increasing order)
   auto fold = [&](int c) {
     const int ln = lane_now();
-    const bool tail = (c + 1) * DC > a.D;
+    // dummy levels past the end (TAIL kernels, last chunk): +inf costs change nothing
+    float kill[2] = {0.0f, 0.0f};
+    if (TAIL && c == a.nch - 1)
+#pragma unroll
+      for (int db = 0; db < 2; db++) kill[db] = c * DC + 16 * db + (ln & 15) >= a.D ? INFINITY : 0.0f;
 #pragma unroll
     for (int xb = 0; xb < 2; xb++)
 #pragma unroll
-      for (int yb = 0; yb < 2; yb++) {
+      for (int yb = 0; yb < NYB; yb++) {
         const f32x4 sq = *(const f32x4*)(srl + (8 * wave + 4 * xb + (ln >> 4)) * TH + 4 * yb);
 #pragma unroll
         for (int db = 0; db < 2; db++) {
@@ -196,7 +212,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
           for (int r = 0; r < 4; r += 2) {
             const f32x2 e = f32x2{E[xb][yb][db][r], E[xb][yb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
             f32x2 cst = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
-            if (tail && dl >= a.D) cst = f32x2{INFINITY, INFINITY};  // dummy level past the end
+            if (TAIL) cst += f32x2{kill[db], kill[db]};  // costs are >= 0: x + 0 = x, x + inf = inf
 #pragma unroll
             for (int h = 0; h < 2; h++) {
               const float cc = cst[h];
@@ -226,7 +242,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
       const int jf = rec[t].txmax - x0 - 1;  // band column of image column -1 (scalar)
       if (jf >= 0 && jf + 1 < 64 + (rec[t].shp >> 16)) {  // inside the band's 64 + span columns
         if (tid < a.pk_pairs) {
-          u32x4* e = nbase + (t & 1) * nbuf + tid * BW + jf;
+          u32x4* e = nbase + (t & 1) * nbuf + tid * BWP + jf;
           const u32x4 v = e[1];
           *e = u32x4{v.x << 8, (v.y << 8) | (v.x >> 24), v.z << 8, (v.w << 8) | (v.z >> 24)};
         }
@@ -236,40 +252,67 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     if (t + 1 < T) stage(t + 1, n1, (t + 1) & 1);
     if (FIRST && cprev >= 0) fold(cprev);
     const u32x4* npk = nbase + (t & 1) * nbuf;
-    const u32x4* nst = npk + a.pk_pairs * BW;
+    const u32x4* nst = npk + a.pk_pairs * BWP;
     const int ln = lane_now();
     const int g = ln >> 4;
     int cl[2];
 #pragma unroll
     for (int db = 0; db < 2; db++) cl[db] = colo_l[t * DC + 16 * db + (ln & 15)];
+    // TH = 4 (room in the registers): a block's two MFMAs issue together and
+    // the next block's B operands are read before this block is finished, so
+    // the LDS and MFMA latencies overlap; TH = 8 (at the 128-VGPR cap): one
+    // level block at a time (the paired form spilled 16-40 B)
+    constexpr bool PF = TH == 4;
+    auto bread = [&](int k, int db) {  // block k = (xb, yb) = (k / NYB, k % NYB)
+      return npk[(2 * (k % NYB) + g) * BWP + 8 * wave + 4 * (k / NYB) + cl[db]];
+    };
+    auto finish = [&](int xb, int yb, int db, const i32x4& acc, const f32x4& nsr) {
+      const int colS = 8 * wave + 4 * xb + cl[db] + g;  // stats band column of this lane's pixel column
+      const f32x4 s0 = __builtin_bit_cast(f32x4, nst[(2 * yb) * BWP + colS]);      // rows 0, 1
+      const f32x4 s1 = __builtin_bit_cast(f32x4, nst[(2 * yb + 1) * BWP + colS]);  // rows 2, 3
 #pragma unroll
-    for (int xb = 0; xb < 2; xb++)
+      for (int p = 0; p < 2; p++) {
+        const f32x4 sv = p ? s1 : s0;
+        const f32x2 f = f32x2{__int_as_float(acc[2 * p]), __int_as_float(acc[2 * p + 1])} - f32x2{kMagicF, kMagicF};
+        const f32x2 xv = __builtin_elementwise_fma(f32x2{nsr[2 * p], nsr[2 * p + 1]}, f32x2{sv.z, sv.w},
+                                                   f * f32x2{sv.x, sv.y});
+        if (FIRST) {
+          E[xb][yb][db][2 * p] = xv.x;
+          E[xb][yb][db][2 * p + 1] = xv.y;
+        } else {
+          E[xb][yb][db][2 * p] = vmax(E[xb][yb][db][2 * p], xv.x);
+          E[xb][yb][db][2 * p + 1] = vmax(E[xb][yb][db][2 * p + 1], xv.y);
+        }
+      }
+    };
+    if (PF) {
+      u32x4 b0 = bread(0, 0), b1 = bread(0, 1);
 #pragma unroll
-      for (int yb = 0; yb < 2; yb++) {
+      for (int k = 0; k < 2 * NYB; k++) {
+        const int xb = k / NYB, yb = k % NYB;
+        const i32x4 acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, b0), bias, 0, 0, 0);
+        const i32x4 acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, b1), bias, 0, 0, 0);
+        if (k + 1 < 2 * NYB) {
+          b0 = bread(k + 1, 0);
+          b1 = bread(k + 1, 1);
+        }
+        const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
+        finish(xb, yb, 0, acc0, nsr);
+        finish(xb, yb, 1, acc1, nsr);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2 * NYB; k++) {
+        const int xb = k / NYB, yb = k % NYB;
         const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
 #pragma unroll
         for (int db = 0; db < 2; db++) {
-          const int colB = 8 * wave + 4 * xb + cl[db];  // pk band column of the block's first pixel column
-          const u32x4 bv = npk[(2 * yb + g) * BW + colB];
-          const i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, bv), bias, 0, 0, 0);
-          const f32x4 s0 = __builtin_bit_cast(f32x4, nst[(2 * yb) * BW + colB + g]);      // rows 0, 1
-          const f32x4 s1 = __builtin_bit_cast(f32x4, nst[(2 * yb + 1) * BW + colB + g]);  // rows 2, 3
-#pragma unroll
-          for (int p = 0; p < 2; p++) {
-            const f32x4 sv = p ? s1 : s0;
-            const f32x2 f = f32x2{__int_as_float(acc[2 * p]), __int_as_float(acc[2 * p + 1])} - f32x2{kMagicF, kMagicF};
-            const f32x2 xv = __builtin_elementwise_fma(f32x2{nsr[2 * p], nsr[2 * p + 1]}, f32x2{sv.z, sv.w},
-                                                       f * f32x2{sv.x, sv.y});
-            if (FIRST) {
-              E[xb][yb][db][2 * p] = xv.x;
-              E[xb][yb][db][2 * p + 1] = xv.y;
-            } else {
-              E[xb][yb][db][2 * p] = vmax(E[xb][yb][db][2 * p], xv.x);
-              E[xb][yb][db][2 * p + 1] = vmax(E[xb][yb][db][2 * p + 1], xv.y);
-            }
-          }
+          const i32x4 acc =
+              __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, bread(k, db)), bias, 0, 0, 0);
+          finish(xb, yb, db, acc, nsr);
         }
       }
+    }
     __syncthreads();  // step t+1's bands landed; this buffer free for t+2
   };
   {
@@ -288,7 +331,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   float* m1 = m0 + 16 * kMfMergeStride;
   int* mi = (int*)(m1 + 16 * kMfMergeStride);
 #pragma unroll
-  for (int yb = 0; yb < 2; yb++) {
+  for (int yb = 0; yb < NYB; yb++) {
     {
       const int ln = lane_now(), cls = ln & 15;
 #pragma unroll
@@ -334,18 +377,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
-template <int BW>
+template <int BW, int TH, bool TAIL>
 int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec* plan, NccArgs& a,
                    const WtaOut& wo, int tmax) {
-  const int variant[8] = {5, 8, 16, 8, BW, kParEven, 1, 2};
+  const int variant[8] = {5, TH, 16, 8, BW, kParEven, 1, 2};
   std::copy(variant, variant + 8, ctx->ncc_last);
   a.tiles_x = (a.W + 63) / 64;
-  a.ntiles = a.tiles_x * ((a.H + 7) / 8);
+  a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);
   a.tiles_per_xcd = (a.nref * a.ntiles + 7) / 8;
   a.nch = (a.D + 31) / 32;
-  const size_t lds = std::max((size_t)2 * 16 * (a.pk_pairs + a.st_pairs) * BW, (size_t)3 * 16 * kMfMergeStride * 4) +
-                     2 * 64 * 8 * 4 + (size_t)tmax * 32 * 2;
-  auto kern = k_ncc_mfma<BW>;
+  const size_t lds = std::max((size_t)2 * 16 * (a.pk_pairs + a.st_pairs) * (BW + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
+                     2 * 64 * TH * 4 + (size_t)tmax * 32 * 2;
+  auto kern = k_ncc_mfma<BW, TH, TAIL>;
   if (lds > 64 * 1024)
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(ncc mfma lds)");
@@ -357,7 +400,7 @@ int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccM
 }  // namespace
 
 // the matrix-core form's plan: one NccMRec per (32-level chunk, neighbour)
-NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx) {
+NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, int TH) {
   constexpr int DC = 32, RW = sizeof(NccMRec) / 4;
   const int nch = (D + DC - 1) / DC;
   NccPlanM p;
@@ -374,8 +417,8 @@ NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx) {
       int32_t* e = p.table.data() + ((size_t)c * nn + n) * RW;
       e[0] = txmax;
       e[1] = 0;
-      e[2] = 6;                          // pk pair rows: y0-2 .. y0+9 (K = 5, TH = 8, no vertical shift)
-      e[3] = 4 | ((txmax - txmin) << 16);  // stats pair rows y0 .. y0+7 | the chunk's column span
+      e[2] = (TH + 4) / 2;                          // pk pair rows: y0-2 .. y0+TH+1 (K = 5, no vertical shift)
+      e[3] = (TH / 2) | ((txmax - txmin) << 16);  // stats pair rows y0 .. y0+TH-1 | the chunk's column span
       int16_t* co = (int16_t*)(e + 4);
       for (int j = 0; j < DC; j++) {
         const int dl = c * DC + j;
@@ -391,11 +434,26 @@ NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx) {
 int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
                     const WtaOut& wo, int bw, int tmax) {
   const NccMRec* pl = (const NccMRec*)plan_dev;
-  return bw <= 64    ? launch_mfma_bw<64>(ctx, stats, pk, pl, a, wo, tmax)
-         : bw <= 80  ? launch_mfma_bw<80>(ctx, stats, pk, pl, a, wo, tmax)
-         : bw <= 96  ? launch_mfma_bw<96>(ctx, stats, pk, pl, a, wo, tmax)
-         : bw <= 128 ? launch_mfma_bw<128>(ctx, stats, pk, pl, a, wo, tmax)
-                     : launch_mfma_bw<192>(ctx, stats, pk, pl, a, wo, tmax);
+  const bool tail = a.D % 32 != 0;
+  if (mfma_tile_rows() == 8) {
+    if (tail) return launch_mfma_bw<192, 8, true>(ctx, stats, pk, pl, a, wo, tmax);
+    return bw <= 128 ? launch_mfma_bw<128, 8, false>(ctx, stats, pk, pl, a, wo, tmax)
+                     : launch_mfma_bw<192, 8, false>(ctx, stats, pk, pl, a, wo, tmax);
+  }
+  if (tail)
+    return bw <= 64    ? launch_mfma_bw<64, 4, true>(ctx, stats, pk, pl, a, wo, tmax)
+           : bw <= 128 ? launch_mfma_bw<128, 4, true>(ctx, stats, pk, pl, a, wo, tmax)
+                       : launch_mfma_bw<192, 4, true>(ctx, stats, pk, pl, a, wo, tmax);
+  return bw <= 64    ? launch_mfma_bw<64, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
+         : bw <= 80  ? launch_mfma_bw<80, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
+         : bw <= 96  ? launch_mfma_bw<96, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
+         : bw <= 128 ? launch_mfma_bw<128, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
+                     : launch_mfma_bw<192, 4, false>(ctx, stats, pk, pl, a, wo, tmax);
+}
+
+int mfma_tile_rows() {
+  const char* e = getenv("MVS_NCC_MFMA_TH");  // read per call (A/B): 4 or 8 (default)
+  return e && atoi(e) == 4 ? 4 : 8;
 }
 
 }  // namespace ncc

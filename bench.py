@@ -11,9 +11,8 @@ hypotheses x 4 neighbours and its winner-take-all + confidence.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--cost ncc|sad]
 
 `value` is the fused step (mvs_ncc_wta_d: the sweep kernel folds the WTA in,
-no cost volume in HBM), with the superpixel chain on a side HIP stream beside
-the per-pixel chain (--serial: one stream; `serial_variant` times that form
-too, and `roofline_sweep` comes from it).  The same invocation also times the two-pass step
+no cost volume in HBM), on one HIP stream (--concurrent: the superpixel chain
+on a side stream; `concurrent_variant` times that form too).  The same invocation also times the two-pass step
 (materialised [D][H][W] volume + the k_wta streaming pass, bit-identical maps):
 `roofline` is k_wta's HBM read of that volume, the north star's roofline.
 
@@ -94,11 +93,9 @@ def parse(argv=None):
     ap.add_argument("--two-pass", action="store_true",
                     help="headline = the two-pass step (cost volume in HBM + k_wta) instead of the fused sweep")
     ap.add_argument("--concurrent", action="store_true",
-                    help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py); "
-                         "the default for the fused NCC headline of the unsharded configs")
-    ap.add_argument("--serial", action="store_true",
-                    help="one stream for the whole step (the fused headline otherwise runs the superpixel "
-                         "chain on a side stream)")
+                    help="superpixel chain on a second stream beside the per-pixel chain (pipeline.py); one "
+                         "stream is the default (`concurrent_variant` times this form beside the headline)")
+    ap.add_argument("--serial", action="store_true", help="one stream (the default; kept for old command lines)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher, rank setup, gathers and max-over-ranks timing on gloo")
     return ap.parse_args(argv)
@@ -401,13 +398,14 @@ def bench(args, world, rank, local):
     def avg(lst):
         return sum(s.elapsed_time(t) for s, t, _ in lst) / len(lst) * 1e-3
 
-    # the fused NCC headline runs the superpixel chain (SLIC, extents,
-    # superpixel sweep) on a side stream beside the per-pixel chain
-    # (pipeline.py, concurrent=True): C2 2.55 -> 2.52 ms per step in three
-    # interleaved rounds (profiles/archive/r03j_concurrent.txt); --serial turns it off
-    # (c3, with refinement and the filter after the join: 3.462-3.469 ->
-    # 3.431-3.434 ms in three interleaved rounds, profiles/archive/r03n_ref_c3.txt)
-    conc_head = args.concurrent or (fused and not sharded and cost == "ncc" and not args.serial)
+    # One HIP stream for the whole step (the default since round 5).  The
+    # superpixel chain on a side stream beside the per-pixel chain
+    # (pipeline.py, concurrent=True; --concurrent) bought 0.05 % in round 4
+    # and 0.2 % with the matrix-core sweep (2.0673 vs 2.0716 ms per C2 step,
+    # profiles/r05/bench_default_conc.json): both chains are throughput-bound,
+    # so sharing the CUs only moves time between them.  Its A/B stays in the
+    # line as `concurrent_variant`.
+    conc_head = bool(args.concurrent)
 
     def make(fz, conc=False):
         p = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,
@@ -448,6 +446,21 @@ def bench(args, world, rank, local):
                       torch.equal(getattr(ser_out, f).view(torch.int32), getattr(out, f).view(torch.int32))
                       for f in ("disp", "conf") if getattr(out, f, None) is not None))}
 
+    conc_var = None
+    if not conc_head and fused and not sharded and cost == "ncc" and world == 1:
+        _, conc_step = make(fused, True)
+        saved = {k: list(v) for k, v in timers.items()}
+        c_el, c_out = timed(conc_step, args.steps, max(1, args.warmup), dev, world, sync)
+        for k in timers:  # the headline's own timers stay the ones of the headline pass
+            timers[k][:] = saved[k]
+        conc_var = {"what": "the same step with the superpixel chain on a side HIP stream beside the per-pixel "
+                            "chain (--concurrent)",
+                    "value": round(units * W * H * args.steps / c_el / 1e6, 3), "unit": "Mpix/s",
+                    "ms_per_step": round(c_el * 1e3 / max(args.steps, 1), 4),
+                    "bit_identical_to_headline": bool(all(
+                        torch.equal(getattr(c_out, f).view(torch.int32), getattr(out, f).view(torch.int32))
+                        for f in ("disp", "conf") if getattr(out, f, None) is not None))}
+
     res = {
         "metric": METRIC,
         "value": round(mpix, 3),
@@ -463,7 +476,7 @@ def bench(args, world, rank, local):
                   "SLIC / superpixel SAD / refinement in f32 with the reference's f64 promotions)") if cost == "ncc"
                  else "f32 (Lab SAD, the reference's arithmetic; f64 where its double literals promote)",
         "data": "synthetic (seeded rendered camera-array stack, RGBx resident in HBM)",
-        "config": {"workload": cfg["workload"] if cost == cfg["cost"] else
+        "config": {"name": args.config, "workload": cfg["workload"] if cost == cfg["cost"] else
                    cfg["workload"].replace("NCC", f"{cost.upper()} (--cost {cost}) instead of NCC"), "views": V, "width": W, "height": H, "hypotheses": D,
                    "window": cfg["K"], "cost": cost, "spixl_size": cfg["S"],
                    "neighbours": int(pipe.cam.subset_num.max()),
@@ -476,6 +489,8 @@ def bench(args, world, rank, local):
     }
     if serial is not None:
         res["serial_variant"] = serial
+    if conc_var is not None:
+        res["concurrent_variant"] = conc_var
     if fused and head_timers["fused"]:
         t_f = avg(head_timers["fused"])  # per call (one run of reference views)
         vpc = sum(n for _, _, n in head_timers["fused"]) / len(head_timers["fused"])
@@ -711,12 +726,12 @@ def c3_subline(args, e, world, sync, check=True):
                          window=c["K"], cost="ncc")
     stack, _ = synth.make_stack(W, H, c["aw"], c["ah"], c["dmin"], c["dmax"], c["bl"], 0x5EED + 2)  # = --config c3
     rgbx = torch.from_numpy(stack).to(e.device)
-    p = Pipeline(e, st, W, H, pixel_cost="ncc", refine=True, filt=True, concurrent=not args.serial, fused=True)
+    p = Pipeline(e, st, W, H, pixel_cost="ncc", refine=True, filt=True, concurrent=bool(args.concurrent), fused=True)
     steps = 5
     el, out = timed(lambda: p.exe_pipeline(rgbx), steps, 1, e.device, world, sync)
     r = {"what": c["workload"], "value": round(V * W * H * steps / el / 1e6, 3), "unit": "Mpix/s",
          "ms_per_step": round(el * 1e3 / steps, 4), "steps": steps,
-         "streams": "one" if args.serial else "superpixel chain on a side stream"}
+         "streams": "superpixel chain on a side stream" if args.concurrent else "one"}
     if check:
         from oracle import oracle as orc
         t0 = time.perf_counter()

@@ -16,7 +16,8 @@ def main():
     c = sqlite3.connect(db)
     acc = collections.OrderedDict()
     for n, s, e in c.execute("select name, start, end from kernels order by start"):
-        n = n.replace("mvs::(anonymous namespace)::", "").replace("void ", "").split("(")[0][:70]
+        n = n.replace("mvs::ncc::(anonymous namespace)::", "").replace("mvs::(anonymous namespace)::", "")
+        n = n.replace("void ", "").split("(")[0][:70]
         if keys and not any(k in n for k in keys):
             continue
         acc.setdefault(n, []).append((e - s) / 1e3)

@@ -64,6 +64,11 @@ __device__ __forceinline__ float vmin(float acc, float e) {
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(e));
   return r;
 }
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 // median of three: with lo <= hi, med3(lo, hi, c) = min(hi, max(lo, c))
 __device__ __forceinline__ float vmed3(float lo, float hi, float c) {
   float r;

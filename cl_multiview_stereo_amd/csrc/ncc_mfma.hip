@@ -110,37 +110,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
   for (int i = tid; i < T * 16; i += NW * 64) ((int*)colo_l)[i] = rec[i >> 4].colo[i & 15];
   stage(0, 0, 0);
   const long zo = (long)a.z[ref] * Pv;
-  // wave 0: -Sr' and s_r of the tile's 64 x TH pixels (lane = column), as k_ncc_volume
-  if (wave == 0) {
-    const int x = x0 + lane, xc = min(x, W - 1);
-    int rsum[NR], rsq[NR];
+  // -Sr' and s_r of the tile's 64 x TH pixels (lane = column), as k_ncc_volume:
+  // wave w takes rows w, w + 8, ... (one correctly rounded sqrt + divide per
+  // row and lane, spread over the waves instead of TH of them on wave 0)
+  for (int o = wave; o < TH; o += NW) {
+    const int x = x0 + lane, xc = min(x, W - 1), y = y0 + o;
+    int s1 = 0, s2 = 0;
 #pragma unroll
-    for (int k = 0; k < NR; k++) {
-      const uint2 v = pk[zo + pair_index(min(max(y0 - R + k, 0), H - 1), xc, W)];
+    for (int k = 0; k < 2 * R + 1; k++) {
+      const uint2 v = pk[zo + pair_index(min(max(y - R + k, 0), H - 1), xc, W)];
       const unsigned lo = v.x, hi = v.y & 0xffu;
-      rsum[k] = dot4(lo, 0x01010101u, dot4(hi, 0x01010101u, 0));
-      rsq[k] = dot4(lo, lo, dot4(hi, hi, 0));
+      s1 = dot4(lo, 0x01010101u, dot4(hi, 0x01010101u, s1));
+      s2 = dot4(lo, lo, dot4(hi, hi, s2));
     }
-    float nsr[TH], sr[TH];
-#pragma unroll
-    for (int o = 0; o < TH; o++) {
-      int s1 = 0, s2 = 0;
-#pragma unroll
-      for (int k = 0; k < 2 * R + 1; k++) {
-        s1 += rsum[o + k];
-        s2 += rsq[o + k];
-      }
-      const int y = y0 + o;
-      const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
-      const int var = NK * s2 - s1 * s1;
-      sr[o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
-      nsr[o] = -(float)s1;
-    }
-#pragma unroll
-    for (int o = 0; o < TH; o += 4) {
-      *(f32x4*)(rsn_l + lane * TH + o) = f32x4{nsr[o], nsr[o + 1], nsr[o + 2], nsr[o + 3]};
-      *(f32x4*)(srl + lane * TH + o) = f32x4{sr[o], sr[o + 1], sr[o + 2], sr[o + 3]};
-    }
+    const bool valid = x - R >= 0 && x + R < W && y - R >= 0 && y + R < H;
+    const int var = NK * s2 - s1 * s1;
+    srl[lane * TH + o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
+    rsn_l[lane * TH + o] = -(float)s1;
   }
   // the reference operands: pixel block (xb, yb) of this wave = columns
   // x0 + 8 wave + 4 xb .. +3, rows y0 + 4 yb .. +3.  Lane l supplies row
@@ -204,24 +190,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
 #pragma unroll
       for (int yb = 0; yb < NYB; yb++) {
         const f32x4 sq = *(const f32x4*)(srl + (8 * wave + 4 * xb + (ln >> 4)) * TH + 4 * yb);
+        // this lane's two levels of the chunk, dl0 < dl1 = dl0 + 16, folded as a
+        // pair: with lo / hi their smaller / larger cost, the triple's new
+        // second smallest is min(max(v0, lo), v1, hi) (the second of the
+        // multiset {v0 <= v1, c0, c1}), its smallest min(v0, lo), and its level
+        // the pair's first argmin (dl1 only if c1 < c0) when lo < v0: the
+        // sequential fold's results in fewer instructions per level
+        const int dl0 = c * DC + (ln & 15);
+        const unsigned d0 = (unsigned)dl0 * 0x10001u, d1 = (unsigned)(dl0 + 16) * 0x10001u;
 #pragma unroll
-        for (int db = 0; db < 2; db++) {
-          const int dl = c * DC + 16 * db + (ln & 15);
-          const unsigned dl2 = (unsigned)dl * 0x10001u;
+        for (int r = 0; r < 4; r += 2) {
+          f32x2 cst[2];
 #pragma unroll
-          for (int r = 0; r < 4; r += 2) {
+          for (int db = 0; db < 2; db++) {
             const f32x2 e = f32x2{E[xb][yb][db][r], E[xb][yb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
-            f32x2 cst = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
-            if (TAIL) cst += f32x2{kill[db], kill[db]};  // costs are >= 0: x + 0 = x, x + inf = inf
+            cst[db] = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
+            if (TAIL) cst[db] += f32x2{kill[db], kill[db]};  // costs are >= 0: x + 0 = x, x + inf = inf
+          }
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-              const float cc = cst[h];
-              const unsigned hm = h ? 0xffff0000u : 0x0000ffffu;
-              unsigned& wp = wi0p[xb][yb][r >> 1];
-              wv1[xb][yb][r + h] = vmed3(wv0[xb][yb][r + h], wv1[xb][yb][r + h], cc);
-              wp = cc < wv0[xb][yb][r + h] ? (wp & ~hm) | (dl2 & hm) : wp;
-              wv0[xb][yb][r + h] = vmin(wv0[xb][yb][r + h], cc);
-            }
+          for (int h = 0; h < 2; h++) {
+            const float c0 = cst[0][h], c1 = cst[1][h];  // never NaN: 1 - max(-1, NaN) = 2
+            const unsigned hm = h ? 0xffff0000u : 0x0000ffffu;
+            unsigned& wp = wi0p[xb][yb][r >> 1];
+            float& v0 = wv0[xb][yb][r + h];
+            float& v1 = wv1[xb][yb][r + h];
+            const float lo = vmin(c0, c1), hi = vmax(c0, c1);
+            const unsigned idx = c1 < c0 ? d1 : d0;
+            v1 = vmin3(vmax(v0, lo), v1, hi);
+            wp = lo < v0 ? (wp & ~hm) | (idx & hm) : wp;
+            v0 = vmin(v0, lo);
           }
         }
       }
@@ -348,13 +345,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
     __syncthreads();
     if (tid < 256) {
       const int q = tid, xx = x0 + (q & 63), yy = y0 + 4 * yb + (q >> 6);
+      // lexicographic (cost, level) minimum; "no level" (-1) compares as the
+      // largest level (it only ever comes with the initial cost 1e6, which no
+      // real level has).  Costs can be slightly negative (NCC rounding past 1),
+      // so they are compared as floats.
       float bv = m0[q];
-      int bi = mi[q];
+      unsigned bi = (unsigned)mi[q];
 #pragma unroll
       for (int w = 1; w < 16; w++) {
         const float v = m0[w * kMfMergeStride + q];
-        const int i = mi[w * kMfMergeStride + q];
-        if (v < bv || (v == bv && i >= 0 && i < bi)) {
+        const unsigned i = (unsigned)mi[w * kMfMergeStride + q];
+        if (v < bv || (v == bv && i < bi)) {
           bv = v;
           bi = i;
         }
@@ -363,13 +364,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
 #pragma unroll
       for (int w = 0; w < 16; w++) {
         const int i = mi[w * kMfMergeStride + q];
-        const float v = (i >= bi - 1 && i <= bi + 1) ? m1[w * kMfMergeStride + q] : m0[w * kMfMergeStride + q];
+        const float v = (unsigned)(i - (int)bi + 1) <= 2u ? m1[w * kMfMergeStride + q] : m0[w * kMfMergeStride + q];
         c2 = vmin(c2, v);
       }
       if (xx < W && yy < H) {
         const long p = P * ref + (long)yy * W + xx;
-        wo.disp[p] = bi >= 0 ? wo.levels[bi] : 0.0f;
-        if (wo.conf) wo.conf[p] = (bi < 0 || c2 == kWtaInit) ? 0.0f : c2 - bv;
+        wo.disp[p] = (int)bi >= 0 ? wo.levels[bi] : 0.0f;
+        if (wo.conf) wo.conf[p] = ((int)bi < 0 || c2 == kWtaInit) ? 0.0f : c2 - bv;
       }
     }
     __syncthreads();

@@ -227,6 +227,12 @@ int mvs_slic_d(mvs_ctx* c, float* lab, int V, int W, int H, const mvs_slic_param
   size_t sb = std::max(mvs::update_scratch_bytes(V, W, H, S),
                        p->enforce_connectivity ? sizeof(uint32_t) * (size_t)V * W * H : (size_t)0);
   if (p->edge_enable) sb = std::max(sb, sizeof(float) * (size_t)V * W * H);
+  // the window-walk update (S % 16 != 0) reads 16-bit copies of the labels
+  // that each assignment writes beside them (labels < 65536); the scratch is
+  // free then (the edge plane is consumed before the first assignment, the
+  // connectivity pass runs after the last)
+  const bool l16 = S % 16 != 0 && p->no_iter > 0 && (long)mvs::map_dim(W, S) * mvs::map_dim(H, S) <= 65536;
+  if (l16) sb = std::max(sb, sizeof(uint16_t) * (size_t)V * W * H);
   int rc = 0;
   void* scr = sb ? mvs::scratch(c, sb, &rc) : nullptr;
   if (rc) return rc;
@@ -244,10 +250,12 @@ int mvs_slic_d(mvs_ctx* c, float* lab, int V, int W, int H, const mvs_slic_param
                                   i + 1 < p->no_iter ? part : nullptr));
     }
   } else {
-    RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels));
+    uint16_t* lb16 = l16 ? (uint16_t*)scr : nullptr;
+    RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels, lb16));
     for (int i = 0; i < p->no_iter; i++) {
-      RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl, part));
-      RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels));
+      RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl, part, lb16));
+      RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels,
+                            i + 1 < p->no_iter ? lb16 : nullptr));
     }
   }
   if (p->enforce_connectivity) {

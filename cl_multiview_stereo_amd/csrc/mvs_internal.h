@@ -69,13 +69,13 @@ int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labe
 int launch_edge_step(hipStream_t s, float* lab, int V, int W, int H, int S, int edge_enable, float* spixl,
                      float* edge);
 int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
-                  float col_n, float weight, int search, uint32_t* labels);
+                  float col_n, float weight, int search, uint32_t* labels, uint16_t* lb16 = nullptr);
 size_t update_scratch_bytes(int V, int W, int H, int S);
 int launch_assign_tiles(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
                         float col_n, float weight, int search, uint32_t* labels, float* part);
 int launch_update_finalize(hipStream_t s, const float* part, int V, int W, int H, int S, float* spixl);
 int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V, int W, int H, int S,
-                  float* spixl, float* part);
+                  float* spixl, float* part, const uint16_t* lb16 = nullptr);
 int launch_suppress(hipStream_t s, const uint32_t* in, uint32_t* out, int V, int W, int H);
 
 int launch_boundary(hipStream_t s, int V, int W, int H, int S, const float* spixl, const uint32_t* labels,

@@ -239,7 +239,8 @@ constexpr int AS_TW = 64, AS_TH = 16, AS_MAXC = 128;
 template <bool S3>
 __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, const float* __restrict__ spixl,
                                                 int W, int H, int S, int mw, int mh, float xy_n, float col_n,
-                                                float weight, uint32_t* __restrict__ labels) {
+                                                float weight, uint32_t* __restrict__ labels,
+                                                uint16_t* __restrict__ lb16) {
   __shared__ float4 cxyla[AS_MAXC];  // (cx, cy, L, a)
   __shared__ float cbb[AS_MAXC];     // b
   const int x0 = blockIdx.x * AS_TW, y0 = blockIdx.y * AS_TH, z = blockIdx.z;
@@ -310,6 +311,7 @@ __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, 
         have = have || take;
       }
     labels[pid] = (uint32_t)min_id;
+    if (lb16) lb16[pid] = (uint16_t)min_id;  // the next k_update's 16-bit copy (mw * mh <= 65536)
   }
 }
 
@@ -395,8 +397,12 @@ __device__ __forceinline__ uint32_t wave_sum2_u32(uint32_t sA, uint32_t sB) {
 // UT = tiles per chunk (below): 4 when the window has many tiles (C5, S = 40:
 // G = 57, update 39.1 -> 38.1 ms per C5 step), 1 for a few (S = 8: G = 3,
 // where the chunk's registers cost more occupancy than the latencies it hides).
-template <int UT>
-__global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, const uint32_t* __restrict__ labels,
+// LT: the label type read -- uint16_t when the previous assignment also wrote
+// a 16-bit copy (every label < 65536): each window pixel's label is read by
+// ~9 superpixels' walks, so halving it takes the C5 update from 3.0x its
+// compulsory bytes to ~1.8x
+template <int UT, typename LT = uint32_t>
+__global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, const LT* __restrict__ labels,
                                                 int W, int H, int S, int mw, int mh, int G, int cpl,
                                                 float* __restrict__ spixl) {
   const int lane = threadIdx.x & 63;
@@ -405,14 +411,14 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
   const int gx = sp % mw, gy = sp / mw;
   const long P = (long)W * H;
   const float4* L = lab + (long)z * P;
-  const uint32_t* I = labels + (long)z * P;
+  const LT* I = labels + (long)z * P;
   const int lx = lane & 15, ly0 = lane >> 4;
   float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   // tiles in chunks of UT: every label of the chunk is gathered before any
   // test, then every member's colour, so a chunk costs two memory latencies
   // instead of two per tile; the trees and the partial sums keep tile order
   for (int t0 = 0; t0 < G; t0 += UT) {
-    uint32_t lb[UT][4];
+    LT lb[UT][4];
     int pix[UT][4], bx[UT], by[UT];
 #pragma unroll
     for (int u = 0; u < UT; u++) {
@@ -433,7 +439,7 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
     for (int u = 0; u < UT; u++)
 #pragma unroll
       for (int m = 0; m < 4; m++) {
-        const bool mem = pix[u][m] >= 0 && lb[u][m] == (uint32_t)sp;
+        const bool mem = pix[u][m] >= 0 && lb[u][m] == (LT)sp;
         c[u][m] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (mem) c[u][m] = L[pix[u][m]];
       }
@@ -445,7 +451,7 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
       bool any = false;
 #pragma unroll
       for (int m = 0; m < 4; m++) {
-        const bool mem = pix[u][m] >= 0 && lb[u][m] == (uint32_t)sp;
+        const bool mem = pix[u][m] >= 0 && lb[u][m] == (LT)sp;
         // x, y, count: one packed integer tree of tile-local fields (as k_assign_tiles)
         pk[m] = mem ? (uint32_t)lx | (uint32_t)(ly0 + 4 * m) << 12 | 1u << 24 : 0u;
         v[m][0] = c[u][m].x;
@@ -1041,11 +1047,12 @@ int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labe
 }
 
 int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
-                  float col_n, float weight, int search, uint32_t* labels) {
+                  float col_n, float weight, int search, uint32_t* labels, uint16_t* lb16) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
   if ((AS_TW / S + 4) * (AS_TH / S + 4) > AS_MAXC) return arg_fail("SLIC assign: spixl_size too small");
   hipLaunchKernelGGL(search ? k_assign<true> : k_assign<false>, dim3((W + AS_TW - 1) / AS_TW, (H + AS_TH - 1) / AS_TH, V), dim3(256), 0, s,
-                     (const float4*)lab, spixl, W, H, S, mw, mh, xy_n, col_n, weight, labels);
+                     (const float4*)lab, spixl, W, H, S, mw, mh, xy_n, col_n, weight, labels,
+                     (long)mw * mh <= 65536 ? lb16 : nullptr);
   MVS_LAUNCH_CHECK("k_assign");
   return 0;
 }
@@ -1087,7 +1094,7 @@ size_t update_scratch_bytes(int V, int W, int H, int S) {
 }
 
 int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V, int W, int H, int S,
-                  float* spixl, float* part) {
+                  float* spixl, float* part, const uint16_t* lb16) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
   int G = (int)__builtin_ceilf((float)(S * S * 9) / (float)(kLocal * kLocal));
   int cpl = S * 3 / kLocal;
@@ -1102,8 +1109,14 @@ int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V
     MVS_LAUNCH_CHECK("k_update_finalize");
     return 0;
   }
-  hipLaunchKernelGGL(G > 4 ? k_update<4> : k_update<1>, dim3((mw * mh + 3) / 4, V), dim3(256), 0, s,
-                     (const float4*)lab, labels, W, H, S, mw, mh, G, cpl, spixl);
+  if (lb16 && (long)mw * mh <= 65536) {  // the 16-bit copy the previous launch_assign wrote
+    auto k16 = G > 4 ? k_update<4, uint16_t> : k_update<1, uint16_t>;
+    hipLaunchKernelGGL(k16, dim3((mw * mh + 3) / 4, V), dim3(256), 0, s, (const float4*)lab, lb16, W, H, S, mw, mh,
+                       G, cpl, spixl);
+  } else {
+    hipLaunchKernelGGL(G > 4 ? k_update<4> : k_update<1>, dim3((mw * mh + 3) / 4, V), dim3(256), 0, s,
+                       (const float4*)lab, labels, W, H, S, mw, mh, G, cpl, spixl);
+  }
   MVS_LAUNCH_CHECK("k_update");
   return 0;
 }

@@ -405,7 +405,7 @@ def bench(args, world, rank, local):
     # profiles/r05/bench_default_conc.json): both chains are throughput-bound,
     # so sharing the CUs only moves time between them.  Its A/B stays in the
     # line as `concurrent_variant`.
-    conc_head = bool(args.concurrent)
+    conc_head = bool(args.concurrent) or os.environ.get("MVS_BENCH_CONCURRENT") == "1"  # (env: interleaved A/B)
 
     def make(fz, conc=False):
         p = Pipeline(e, st, W, H, view_subset=vlists, pixel_cost=None if cost == "none" else cost,

@@ -606,9 +606,13 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
   dim3 g(8 * a.tiles_per_xcd);
   auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, PAR, false, NB> : k_ncc_volume<K, TH, DPW, NW, BW, PAR, true, NB>;
   if (!vol) lds = std::max(lds, (size_t)3 * 4 * NW * TH * 64) + 4 * TH * 64;  // WTA partials; + s_r [64][TH]
-  if (lds > 64 * 1024)
+  // per instantiation and form (volume / fused): raise the limit once, not on every launch
+  static size_t lds_set[2] = {64 * 1024, 64 * 1024};
+  if (lds > lds_set[vol ? 0 : 1]) {
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(ncc lds)");
+    lds_set[vol ? 0 : 1] = lds;
+  }
   hipLaunchKernelGGL(kern, g, dim3(NW * 64), lds, s, stats, pk, plan, a, vol, wo);
   MVS_LAUNCH_CHECK(vol ? "k_ncc_volume" : "k_ncc_volume (fused WTA)");
   return 0;

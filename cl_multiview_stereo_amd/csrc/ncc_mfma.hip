@@ -390,9 +390,12 @@ int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccM
   const size_t lds = std::max((size_t)2 * 16 * (a.pk_pairs + a.st_pairs) * (BW + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
                      2 * 64 * TH * 4 + (size_t)tmax * 32 * 2;
   auto kern = k_ncc_mfma<BW, TH, TAIL>;
-  if (lds > 64 * 1024)
+  static size_t lds_set = 64 * 1024;  // per instantiation: raise the limit once, not on every launch
+  if (lds > lds_set) {
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
             "hipFuncSetAttribute(ncc mfma lds)");
+    lds_set = lds;
+  }
   hipLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(512), lds, ctx->stream, stats, pk, plan, a, wo);
   MVS_LAUNCH_CHECK("k_ncc_mfma (fused WTA)");
   return 0;

@@ -771,15 +771,23 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   if (n <= 0) return 0;
   std::vector<NccChoice> ch(n);
   std::vector<std::array<int, kMaxNbr>> views(n);
-  // the matrix-core form (k_ncc_mfma) for fused K = 5 views whose neighbours
-  // are all horizontal (every vertical shift 0) and whose bands leave two
-  // workgroups per CU; MVS_NCC_MFMA=0 (read per call) or a forced variant
-  // (mvs_set_ncc_variant) keeps the scalar kernels
+  // the matrix-core form (k_ncc_mfma) for fused K = 5 views: horizontal lists
+  // (every vertical shift 0) in 32-level double-buffered chunks; lists with
+  // vertical / diagonal neighbours (VERT) in the first of 32-level double- /
+  // single-buffered, 16-level double- / single-buffered chunks whose bands
+  // leave two workgroups per CU (80 KB).  MVS_NCC_MFMA=0 (read per call) or a
+  // forced variant (mvs_set_ncc_variant) keeps the scalar kernels.  VERT
+  // lists take the matrix-core form only with MVS_NCC_MFMA_V=1 (that choice)
+  // or 22 | 21 | 12 | 11 (chunk blocks, buffers: that form): C4's tall bands
+  // keep it DMA-bound and slower than the scalar kernels
   const char* mfe = getenv("MVS_NCC_MFMA");
+  const char* mfv = getenv("MVS_NCC_MFMA_V");
   const bool mf_on = !vol && K == 5 && !(mfe && atoi(mfe) == 0) && !ctx->ncc_nw && !ctx->ncc_dpw && !ctx->ncc_general &&
                      !ctx->ncc_bw;
+  const int mfv_form = mfv ? atoi(mfv) : 0;  // 0: off, 1: automatic, else the form
   std::vector<char> mf(n, 0);
   std::vector<NccPlanM> mplan(n);
+  std::vector<int> mnb(n, 2);
   for (int r = 0; r < n; r++) {
     const int z = z0 + r, nn = sn_host[z];
     if (nn > kMaxNbr) return arg_fail("NCC sweep supports at most 16 neighbours per reference view");
@@ -795,11 +803,28 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
       if (fdy[k] != 0.0f) horiz = false;
     }
     if (mf_on && horiz && nn > 0) {
-      mplan[r] = make_plan_mfma(levels_host, D, nn, fdx, mfma_tile_rows());
+      mplan[r] = make_plan_mfma(levels_host, D, nn, fdx, fdy, bl, 2);
       if (mplan[r].band_w <= 192) {
         mf[r] = 1;
         continue;
       }
+    }
+    if (mf_on && !horiz && nn > 0 && mfv_form != 0) {
+      static const int forms[4][2] = {{2, 2}, {2, 1}, {1, 2}, {1, 1}};
+      for (const auto& f : forms) {
+        const bool forced = mfv_form > 1;
+        if (forced && mfv_form != 10 * f[0] + f[1]) continue;
+        NccPlanM pm = make_plan_mfma(levels_host, D, nn, fdx, fdy, bl, f[0]);
+        const int tm = ((D + 16 * f[0] - 1) / (16 * f[0])) * nn;
+        const size_t cap = forced ? (size_t)160 * 1024 : (size_t)80 * 1024;
+        if (pm.band_w <= 128 && mfma_lds_bytes(pm, pm.band_w, f[1], tm, D) <= cap) {
+          mplan[r] = std::move(pm);
+          mnb[r] = f[1];
+          mf[r] = 1;
+          break;
+        }
+      }
+      if (mf[r]) continue;
     }
     const bool ok = K == 5 ? choose_variant<5>(ctx, levels_host, D, nn, fdx, fdy, bl, ch[r])
                            : choose_variant<7>(ctx, levels_host, D, nn, fdx, fdy, bl, ch[r]);
@@ -813,19 +838,26 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   const char* re = getenv("MVS_NCC_RUN");
   const int maxrun = re ? std::max(1, std::min(kMaxRef, atoi(re))) : kMaxRef;
   for (int i = 0; i < n;) {
-    if (mf[i]) {  // a run of matrix-core views: one launch, the widest band
+    if (mf[i]) {  // a run of matrix-core views of one form: one launch, the widest band, the tallest bands
+      const bool vert = mplan[i].vert;
+      const int ndb = mplan[i].ndb, nb = mnb[i];
       int j = i, bw = 0, tmax = 0;
       NccArgs a{};
       a.W = W;
       a.H = H;
       a.D = D;
-      a.pk_pairs = (mfma_tile_rows() + 4) / 2;
-      a.st_pairs = mfma_tile_rows() / 2;
       std::vector<int32_t> table;
-      while (j < n && mf[j] && j - i < maxrun) {
+      NccPlanM run;  // the run's band extents (LDS check)
+      run.ndb = ndb;
+      while (j < n && mf[j] && j - i < maxrun && mplan[j].vert == vert && mplan[j].ndb == ndb && mnb[j] == nb) {
         const int z = z0 + j;
-        bw = std::max(bw, mplan[j].band_w);
-        tmax = std::max(tmax, ((D + 31) / 32) * sn_host[z]);
+        run.pk_pairs = std::max(run.pk_pairs, mplan[j].pk_pairs);
+        run.st_pairs = std::max(run.st_pairs, mplan[j].st_pairs);
+        const int bw2 = std::max(bw, mplan[j].band_w);
+        const int tm2 = std::max(tmax, ((D + 16 * ndb - 1) / (16 * ndb)) * sn_host[z]);
+        if (vert && j > i && mfma_lds_bytes(run, bw2, nb, tm2, D) > 80 * 1024) break;
+        bw = bw2;
+        tmax = tm2;
         a.z[j - i] = z;
         a.nn[j - i] = sn_host[z];
         a.plan[j - i] = (int)(table.size() / 32);  // 128-B NccMRec records
@@ -834,11 +866,17 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
         j++;
       }
       a.nref = j - i;
+      a.pk_pairs = 0;
+      a.st_pairs = 0;
+      for (int r = i; r < j; r++) {
+        a.pk_pairs = std::max(a.pk_pairs, mplan[r].pk_pairs);
+        a.st_pairs = std::max(a.st_pairs, mplan[r].st_pairs);
+      }
       int rc = 0;
       const int32_t* dev = plan_upload(ctx, table, &rc);
       if (rc) return rc;
       const WtaOut wo{levels_dev, disp + P * i, conf ? conf + P * i : nullptr};
-      rc = launch_ncc_mfma(ctx, stats, pk, dev, a, wo, bw, tmax);
+      rc = launch_ncc_mfma(ctx, stats, pk, dev, a, wo, bw, tmax, vert, ndb, nb);
       if (rc) return rc;
       i = j;
       continue;

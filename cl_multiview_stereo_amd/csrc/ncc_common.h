@@ -167,15 +167,21 @@ __device__ __forceinline__ int dot4(unsigned a, unsigned b, int c) {
 }
 
 // the matrix-core fused sweep (ncc_mfma.hip): its plan (one 128-B record per
-// 32-level chunk and neighbour) and one launch over a run of reference views
+// chunk of 16 NDB levels and neighbour) and one launch over a run of
+// reference views.  vert: some neighbour shifts rows (the general form:
+// per-level band rows, pair reads split at odd offsets); NB: band buffers
 struct NccPlanM {
   std::vector<int32_t> table;
-  int band_w = 0;  // columns per band pair row: 64 + the widest chunk span
+  int band_w = 0;                // columns per band pair row: 64 + the widest chunk span
+  int pk_pairs = 0, st_pairs = 0;  // band heights in row pairs (the tallest step)
+  int ndb = 2;                   // 16-level blocks per chunk
+  bool vert = false;
 };
-NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, int TH);
-int mfma_tile_rows();  // 8 (default) or 4 (MVS_NCC_MFMA_TH=4)
+NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl, int ndb);
+// the LDS bytes of one workgroup of the matrix-core form
+size_t mfma_lds_bytes(const NccPlanM& p, int band_w, int nb, int tmax, int D);
 int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
-                    const WtaOut& wo, int bw, int tmax);
+                    const WtaOut& wo, int bw, int tmax, bool vert, int ndb, int nb);
 
 }  // namespace ncc
 }  // namespace mvs

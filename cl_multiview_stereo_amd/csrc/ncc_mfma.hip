@@ -1,7 +1,7 @@
-// Matrix-core form of the fused NCC sweep + WTA (K = 5, horizontal
-// neighbours): the definition and the outputs are ncc.hip's (k_ncc_volume
-// with FUSE), bit for bit; launch_ncc_refs (ncc.hip) picks it per reference
-// view.  See the comment at NccMRec for the formulation.
+// Matrix-core form of the fused NCC sweep + WTA (K = 5): the definition and
+// the outputs are ncc.hip's (k_ncc_volume with FUSE), bit for bit;
+// launch_ncc_refs (ncc.hip) picks it per reference view.  See the comment at
+// NccMRec for the formulation.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -12,7 +12,7 @@ namespace mvs {
 namespace ncc {
 namespace {
 
-// ---- matrix-core form of the fused sweep (K = 5, horizontal neighbours) ----
+// ---- matrix-core form of the fused sweep (K = 5) ----
 //
 // The correlation Srp'(x, y, d) = sum_{j, i} r'(x+i, y+j) p'(x+i-tx(d), y+j)
 // as a GEMM whose output lands in the SAME (pixel, level) layout for every
@@ -40,24 +40,39 @@ namespace {
 // Lane l holds the levels of class l & 15 (16 apart): the fold keeps the same
 // (smallest, its level, second smallest) triple per cell, and the 16 classes
 // of a pixel are merged through LDS as the scalar kernel merges its waves.
+//
+// VERT (lists with vertical / diagonal neighbours, C4): level j also shifts
+// rows by ty(j), so its footprint starts o_j = tymax - ty(j) + (tymax & 1)
+// rows into the band (the pk and stats bands start o_j's parity apart from
+// a pair boundary alike).  At an odd o_j a lane's two footprint rows (and a
+// pixel's stats rows) straddle two band pair entries: the B operand is two
+// ds_read_b64 (row 2g + o_j, row 2g + o_j + 1) and the stats four (a, b)
+// pairs, per-lane addresses fixed for the step -- the MFMA and the finish
+// are unchanged.  The bands are staged per step (their rows depend on the
+// step's tymax), 16 NDB levels per chunk.
 struct alignas(128) NccMRec {
-  int txmax, tymax;  // band origin, as NccRec (tymax = 0: every shift horizontal)
+  int txmax, tymax;  // band origin, as NccRec
   int bhp, shp;      // pk / stats pair rows to stage | (column span) << 16, as NccRec
   int colo[16];      // 32 x int16: per level j of the chunk, txmax - tx(j) (band column of reference column x0)
+                     // | o_j << 8 (VERT: band row of the level's footprint)
   int pad[12];
 };
 static_assert(sizeof(NccMRec) == 128, "one 128-B record per (chunk, neighbour)");
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int kMfMergeStride = 257;  // LDS merge rows: 256 pixels + 1 (16 classes on distinct banks)
 
-// TH: tile rows (4: a wave owns 8 columns x 4 rows = 2 pixel blocks; 8: 8 x 8 =
-// 4 blocks, twice the per-lane state).  TAIL: D % 32 != 0, the last chunk
-// carries dummy levels past the end.
-template <int BW, int TH, bool TAIL>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5 : 4))) void k_ncc_mfma(
+// A tile is 64 columns x 8 rows: a wave owns 8 columns x 8 rows = 4 pixel
+// blocks.  TAIL: D % DC != 0, the last chunk carries dummy levels past the
+// end.  NDB: 16-level blocks per chunk (DC = 16 NDB levels per step).  NB:
+// band buffers (2: step t+1's bands land while step t computes; 1: staged at
+// the start of each step, the other resident workgroup computing meanwhile).
+template <int BW, bool TAIL, bool VERT, int NDB, int NB>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_mfma(
     const uint2* __restrict__ stats, const uint2* __restrict__ pk, const NccMRec* __restrict__ plan, NccArgs a,
     WtaOut wo) {
-  constexpr int R = 2, NW = 8, DC = 32, NK = 25, NR = TH + 2 * R, NYB = TH / 4;  // NYB: pixel-block rows
+  static_assert(NDB == 1 || NDB == 2, "one or two 16-level blocks per chunk");
+  static_assert(VERT || (NDB == 2 && NB == 2), "the horizontal form: 32-level chunks, double-buffered");
+  constexpr int R = 2, NW = 8, TH = 8, DC = 16 * NDB, NK = 25, NYB = TH / 4;  // NYB: pixel-block rows
   // band row pitch: BW + 1 columns of 16 B, so a lane group's B reads in two
   // rows (row pairs g, g + 1) fall on different banks when the shift per level
   // is even (|dx| = 2: conflict-free instead of 2-way)
@@ -65,10 +80,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
   extern __shared__ __align__(16) uint8_t smem[];
   const int nbuf = (a.pk_pairs + a.st_pairs) * BWP;  // uint4 per neighbour buffer
   u32x4* nbase = (u32x4*)smem;                      // 2 x {npk[pk_pairs][BW], nst[st_pairs][BW]}
-  const int band_bytes = max(2 * nbuf * 16, 3 * 16 * kMfMergeStride * 4);
+  const int band_bytes = max(NB * nbuf * 16, 3 * 16 * kMfMergeStride * 4);
   float* rsn_l = (float*)(smem + band_bytes);  // [64][TH] -Sr' of the tile's pixels (column-major)
   float* srl = rsn_l + 64 * TH;                 // [64][TH] s_r
-  short* colo_l = (short*)(srl + 64 * TH);      // [T][32] band column offsets per step and level
+  short* colo_l = (short*)(srl + 64 * TH);      // [T][DC] band column (| row) offsets per step and level
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int W = a.W, H = a.H;
@@ -85,9 +100,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
   const NccMRec* rec = plan + a.plan[ref];
 
   // LDS-DMA staging of step t's bands (k_ncc_volume's stage, one record per
-  // step).  Every shift is horizontal, so a step's band rows are the same
-  // image rows for every step: wave w stages pk pair row w (w < bhp) and stats
-  // pair row w (w < shp), whose clamped row offsets are computed once per tile
+  // step).  Horizontal lists: every step's band rows are the same image rows,
+  // so wave w stages pk pair row w (w < bhp) and stats pair row w (w < shp),
+  // whose clamped row offsets are computed once per tile.  VERT: the rows
+  // start at the step's tymax, the waves take the pair rows in turn
   const int bhp = (TH + 4) / 2, shp = TH / 2;
   const long pk_row = 2L * W * min(max((y0 - R) / 2 + wave, 0), Hp2 - 1);  // (y0 - R) even: y0 even, R = 2
   const long st_row = 2L * W * min(max(y0 / 2 + wave, 0), Hp2 - 1);
@@ -98,16 +114,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
     u32x4* npk = nbase + b * nbuf;
     u32x4* nst = npk + a.pk_pairs * BWP;
     const int xb0 = x0 - e.txmax + lane;
-    for (int cb = 0; cb < nblk; cb++) {
-      const int c0 = min(cb * 64, span);
-      const int xx = min(max(xb0 + c0, 0), W - 1);
-      if (wave < bhp) glds_b128(pk + vo + pk_row + 2 * xx, npk + wave * BWP + c0);
-      if (wave < shp) glds_b128(stats + vo + st_row + 2 * xx, nst + wave * BWP + c0);
+    if constexpr (!VERT) {
+      for (int cb = 0; cb < nblk; cb++) {
+        const int c0 = min(cb * 64, span);
+        const int xx = min(max(xb0 + c0, 0), W - 1);
+        if (wave < bhp) glds_b128(pk + vo + pk_row + 2 * xx, npk + wave * BWP + c0);
+        if (wave < shp) glds_b128(stats + vo + st_row + 2 * xx, nst + wave * BWP + c0);
+      }
+    } else {
+      const int ebh = e.bhp, esh = e.shp & 0xffff;
+      const int pm0 = (y0 - R - e.tymax) >> 1, sm0 = (y0 - e.tymax) >> 1;  // floor: arithmetic shifts
+      for (int cb = 0; cb < nblk; cb++) {
+        const int c0 = min(cb * 64, span);
+        const int xx = min(max(xb0 + c0, 0), W - 1);
+        const uint2* gpk = pk + vo + 2 * xx;
+        const uint2* gst = stats + vo + 2 * xx;
+        for (int i = wave; i < ebh; i += NW) glds_b128(gpk + 2L * W * min(max(pm0 + i, 0), Hp2 - 1), npk + i * BWP + c0);
+        for (int i = wave; i < esh; i += NW) glds_b128(gst + 2L * W * min(max(sm0 + i, 0), Hp2 - 1), nst + i * BWP + c0);
+      }
     }
   };
 
   // the steps' level -> band column offsets, into LDS (before the pipeline)
-  for (int i = tid; i < T * 16; i += NW * 64) ((int*)colo_l)[i] = rec[i >> 4].colo[i & 15];
+  for (int i = tid; i < T * DC / 2; i += NW * 64) ((int*)colo_l)[i] = rec[i / (DC / 2)].colo[i % (DC / 2)];
   stage(0, 0, 0);
   const long zo = (long)a.z[ref] * Pv;
   // -Sr' and s_r of the tile's 64 x TH pixels (lane = column), as k_ncc_volume:
@@ -160,7 +189,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
   }
   __syncthreads();
 
-  float E[2][NYB][2][4];  // [xb][yb][level block][row]: max over the neighbours so far
+  float E[2][NYB][NDB][4];  // [xb][yb][level block][row]: max over the neighbours so far
   float wv0[2][NYB][4], wv1[2][NYB][4];
   unsigned wi0p[2][NYB][2];  // level of the smallest, rows (2p, 2p+1) as the halves of one register (0xffff: none)
 #pragma unroll
@@ -177,48 +206,57 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
   const i32x4 bias = i32x4{kMagicI, kMagicI, kMagicI, kMagicI};
 
   // fold chunk c's levels into the per-cell triples (k_ncc_volume's fold; this
-  // lane's levels are c * 32 + 16 db + (l & 15), in increasing order)
+  // lane's levels are c * DC + 16 db + (l & 15), in increasing order)
   auto fold = [&](int c) {
     const int ln = lane_now();
     // dummy levels past the end (TAIL kernels, last chunk): +inf costs change nothing
-    float kill[2] = {0.0f, 0.0f};
+    float kill[NDB];
+#pragma unroll
+    for (int db = 0; db < NDB; db++) kill[db] = 0.0f;
     if (TAIL && c == a.nch - 1)
 #pragma unroll
-      for (int db = 0; db < 2; db++) kill[db] = c * DC + 16 * db + (ln & 15) >= a.D ? INFINITY : 0.0f;
+      for (int db = 0; db < NDB; db++) kill[db] = c * DC + 16 * db + (ln & 15) >= a.D ? INFINITY : 0.0f;
 #pragma unroll
     for (int xb = 0; xb < 2; xb++)
 #pragma unroll
       for (int yb = 0; yb < NYB; yb++) {
         const f32x4 sq = *(const f32x4*)(srl + (8 * wave + 4 * xb + (ln >> 4)) * TH + 4 * yb);
-        // this lane's two levels of the chunk, dl0 < dl1 = dl0 + 16, folded as a
-        // pair: with lo / hi their smaller / larger cost, the triple's new
-        // second smallest is min(max(v0, lo), v1, hi) (the second of the
-        // multiset {v0 <= v1, c0, c1}), its smallest min(v0, lo), and its level
-        // the pair's first argmin (dl1 only if c1 < c0) when lo < v0: the
+        // NDB = 2: this lane's two levels of the chunk, dl0 < dl1 = dl0 + 16,
+        // folded as a pair: with lo / hi their smaller / larger cost, the
+        // triple's new second smallest is min(max(v0, lo), v1, hi) (the second
+        // of the multiset {v0 <= v1, c0, c1}), its smallest min(v0, lo), and its
+        // level the pair's first argmin (dl1 only if c1 < c0) when lo < v0: the
         // sequential fold's results in fewer instructions per level
         const int dl0 = c * DC + (ln & 15);
         const unsigned d0 = (unsigned)dl0 * 0x10001u, d1 = (unsigned)(dl0 + 16) * 0x10001u;
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {
-          f32x2 cst[2];
+          f32x2 cst[NDB];
 #pragma unroll
-          for (int db = 0; db < 2; db++) {
+          for (int db = 0; db < NDB; db++) {
             const f32x2 e = f32x2{E[xb][yb][db][r], E[xb][yb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
             cst[db] = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
             if (TAIL) cst[db] += f32x2{kill[db], kill[db]};  // costs are >= 0: x + 0 = x, x + inf = inf
           }
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            const float c0 = cst[0][h], c1 = cst[1][h];  // never NaN: 1 - max(-1, NaN) = 2
             const unsigned hm = h ? 0xffff0000u : 0x0000ffffu;
             unsigned& wp = wi0p[xb][yb][r >> 1];
             float& v0 = wv0[xb][yb][r + h];
             float& v1 = wv1[xb][yb][r + h];
-            const float lo = vmin(c0, c1), hi = vmax(c0, c1);
-            const unsigned idx = c1 < c0 ? d1 : d0;
-            v1 = vmin3(vmax(v0, lo), v1, hi);
-            wp = lo < v0 ? (wp & ~hm) | (idx & hm) : wp;
-            v0 = vmin(v0, lo);
+            if constexpr (NDB == 2) {
+              const float c0 = cst[0][h], c1 = cst[NDB - 1][h];  // never NaN: 1 - max(-1, NaN) = 2
+              const float lo = vmin(c0, c1), hi = vmax(c0, c1);
+              const unsigned idx = c1 < c0 ? d1 : d0;
+              v1 = vmin3(vmax(v0, lo), v1, hi);
+              wp = lo < v0 ? (wp & ~hm) | (idx & hm) : wp;
+              v0 = vmin(v0, lo);
+            } else {  // one level: the sequential fold
+              const float cc = cst[0][h];
+              v1 = vmed3(v0, v1, cc);
+              wp = cc < v0 ? (wp & ~hm) | (d0 & hm) : wp;
+              v0 = vmin(v0, cc);
+            }
           }
         }
       }
@@ -229,6 +267,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
   auto step = [&](int t, int n, int cprev, auto first) {
     constexpr bool FIRST = decltype(first)::value;
     const int n1 = n + 1 == nn ? 0 : n + 1;
+    if (NB == 1 && t > 0) {  // this step's bands into the one buffer (step 0's: before the loop)
+      stage(t, n, 0);
+      __syncthreads();  // vmcnt(0): landed, for every wave
+    }
+    u32x4* const nbuf_t = nbase + (NB == 2 ? (t & 1) * nbuf : 0);
     // A block's B entry sits at column x0b - tx, up to 3 columns left of its
     // cells' neighbour pixels: a valid cell (neighbour column 2, xx = 3) reads
     // the entry of image column -1, which the clamped DMA filled with column
@@ -239,34 +282,61 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
       const int jf = rec[t].txmax - x0 - 1;  // band column of image column -1 (scalar)
       if (jf >= 0 && jf + 1 < 64 + (rec[t].shp >> 16)) {  // inside the band's 64 + span columns
         if (tid < a.pk_pairs) {
-          u32x4* e = nbase + (t & 1) * nbuf + tid * BWP + jf;
+          u32x4* e = nbuf_t + tid * BWP + jf;
           const u32x4 v = e[1];
           *e = u32x4{v.x << 8, (v.y << 8) | (v.x >> 24), v.z << 8, (v.w << 8) | (v.z >> 24)};
         }
         __syncthreads();
       }
     }
-    if (t + 1 < T) stage(t + 1, n1, (t + 1) & 1);
+    if (NB == 2 && t + 1 < T) stage(t + 1, n1, (t + 1) & 1);
     if (FIRST && cprev >= 0) fold(cprev);
-    const u32x4* npk = nbase + (t & 1) * nbuf;
+    const u32x4* npk = nbuf_t;
     const u32x4* nst = npk + a.pk_pairs * BWP;
     const int ln = lane_now();
     const int g = ln >> 4;
-    int cl[2];
+    // per level block: the band column of the lane's level (horizontal), or
+    // (VERT) the lane's B-row and stats-row addresses for block (0, 0): uint2
+    // index of footprint rows o + 2g, o + 2g + 1 and float index of the a of
+    // pixel rows o, o + 1 (b two floats on; rows + 2: the next pair row)
+    int cl[NDB], iB0[NDB], iB1[NDB], iS0[NDB], iS1[NDB];
 #pragma unroll
-    for (int db = 0; db < 2; db++) cl[db] = colo_l[t * DC + 16 * db + (ln & 15)];
-    // TH = 4 (room in the registers): a block's two MFMAs issue together and
-    // the next block's B operands are read before this block is finished, so
-    // the LDS and MFMA latencies overlap; TH = 8 (at the 128-VGPR cap): one
-    // level block at a time (the paired form spilled 16-40 B)
-    constexpr bool PF = TH == 4;
-    auto bread = [&](int k, int db) {  // block k = (xb, yb) = (k / NYB, k % NYB)
-      return npk[(2 * (k % NYB) + g) * BWP + 8 * wave + 4 * (k / NYB) + cl[db]];
+    for (int db = 0; db < NDB; db++) {
+      const int v = colo_l[t * DC + 16 * db + (ln & 15)];
+      if constexpr (!VERT) {
+        cl[db] = v;
+      } else {
+        const int col = 8 * wave + (v & 0xff), o = v >> 8;
+        const int r0 = o + 2 * g, r1 = r0 + 1, s1 = o + 1;
+        iB0[db] = 2 * ((r0 >> 1) * BWP + col) + (r0 & 1);
+        iB1[db] = 2 * ((r1 >> 1) * BWP + col) + (r1 & 1);
+        iS0[db] = 4 * ((o >> 1) * BWP + col + g) + (o & 1);
+        iS1[db] = 4 * ((s1 >> 1) * BWP + col + g) + (s1 & 1);
+      }
+    }
+    auto bread = [&](int xb, int yb, int db) -> i32x4 {
+      if constexpr (!VERT) {
+        return __builtin_bit_cast(i32x4, npk[(2 * yb + g) * BWP + 8 * wave + 4 * xb + cl[db]]);
+      } else {
+        const uint2* b2 = (const uint2*)npk;
+        const int off = 2 * (2 * yb * BWP + 4 * xb);
+        const uint2 lo = b2[iB0[db] + off], hi = b2[iB1[db] + off];
+        return i32x4{(int)lo.x, (int)lo.y, (int)hi.x, (int)hi.y};
+      }
     };
     auto finish = [&](int xb, int yb, int db, const i32x4& acc, const f32x4& nsr) {
-      const int colS = 8 * wave + 4 * xb + cl[db] + g;  // stats band column of this lane's pixel column
-      const f32x4 s0 = __builtin_bit_cast(f32x4, nst[(2 * yb) * BWP + colS]);      // rows 0, 1
-      const f32x4 s1 = __builtin_bit_cast(f32x4, nst[(2 * yb + 1) * BWP + colS]);  // rows 2, 3
+      f32x4 s0, s1;  // {a, a, b, b} of pixel rows 0, 1 and rows 2, 3 of the block
+      if constexpr (!VERT) {
+        const int colS = 8 * wave + 4 * xb + cl[db] + g;  // stats band column of this lane's pixel column
+        s0 = __builtin_bit_cast(f32x4, nst[(2 * yb) * BWP + colS]);
+        s1 = __builtin_bit_cast(f32x4, nst[(2 * yb + 1) * BWP + colS]);
+      } else {
+        const float* f = (const float*)nst;
+        const int off = 4 * (2 * yb * BWP + 4 * xb);
+        const int q0 = iS0[db] + off, q1 = iS1[db] + off, q2 = q0 + 4 * BWP, q3 = q1 + 4 * BWP;
+        s0 = f32x4{f[q0], f[q1], f[q0 + 2], f[q1 + 2]};
+        s1 = f32x4{f[q2], f[q3], f[q2 + 2], f[q3 + 2]};
+      }
 #pragma unroll
       for (int p = 0; p < 2; p++) {
         const f32x4 sv = p ? s1 : s0;
@@ -282,35 +352,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
         }
       }
     };
-    if (PF) {
-      u32x4 b0 = bread(0, 0), b1 = bread(0, 1);
+    // one level block at a time (at the 128-VGPR cap the paired form spilled 16-40 B)
 #pragma unroll
-      for (int k = 0; k < 2 * NYB; k++) {
-        const int xb = k / NYB, yb = k % NYB;
-        const i32x4 acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, b0), bias, 0, 0, 0);
-        const i32x4 acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, b1), bias, 0, 0, 0);
-        if (k + 1 < 2 * NYB) {
-          b0 = bread(k + 1, 0);
-          b1 = bread(k + 1, 1);
-        }
-        const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
-        finish(xb, yb, 0, acc0, nsr);
-        finish(xb, yb, 1, acc1, nsr);
-      }
-    } else {
+    for (int k = 0; k < 2 * NYB; k++) {
+      const int xb = k / NYB, yb = k % NYB;
+      const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
 #pragma unroll
-      for (int k = 0; k < 2 * NYB; k++) {
-        const int xb = k / NYB, yb = k % NYB;
-        const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
-#pragma unroll
-        for (int db = 0; db < 2; db++) {
-          const i32x4 acc =
-              __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], __builtin_bit_cast(i32x4, bread(k, db)), bias, 0, 0, 0);
-          finish(xb, yb, db, acc, nsr);
-        }
+      for (int db = 0; db < NDB; db++) {
+        const i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], bread(xb, yb, db), bias, 0, 0, 0);
+        finish(xb, yb, db, acc, nsr);
       }
     }
-    __syncthreads();  // step t+1's bands landed; this buffer free for t+2
+    __syncthreads();  // NB = 2: step t+1's bands landed, this buffer free for t+2; NB = 1: free for t+1
   };
   {
     int t = 0;
@@ -378,18 +431,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TH == 4 ? 5
 }
 
 
-template <int BW, int TH, bool TAIL>
+template <int BW, bool TAIL, bool VERT, int NDB, int NB>
 int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec* plan, NccArgs& a,
                    const WtaOut& wo, int tmax) {
-  const int variant[8] = {5, TH, 16, 8, BW, kParEven, 1, 2};
+  constexpr int TH = 8, DC = 16 * NDB;
+  const int variant[8] = {5, TH, DC, 8, BW, VERT ? kParMixed : kParEven, 1, NB};
   std::copy(variant, variant + 8, ctx->ncc_last);
   a.tiles_x = (a.W + 63) / 64;
   a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);
   a.tiles_per_xcd = (a.nref * a.ntiles + 7) / 8;
-  a.nch = (a.D + 31) / 32;
-  const size_t lds = std::max((size_t)2 * 16 * (a.pk_pairs + a.st_pairs) * (BW + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
-                     2 * 64 * TH * 4 + (size_t)tmax * 32 * 2;
-  auto kern = k_ncc_mfma<BW, TH, TAIL>;
+  a.nch = (a.D + DC - 1) / DC;
+  const size_t lds = std::max((size_t)NB * 16 * (a.pk_pairs + a.st_pairs) * (BW + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
+                     2 * 64 * TH * 4 + (size_t)tmax * DC * 2;
+  auto kern = k_ncc_mfma<BW, TAIL, VERT, NDB, NB>;
   static size_t lds_set = 64 * 1024;  // per instantiation: raise the limit once, not on every launch
   if (lds > lds_set) {
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -401,63 +455,90 @@ int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccM
   return 0;
 }
 
+// the band pitch template a VERT launch takes
+int vert_bw(int band_w, bool tail) { return tail ? 128 : band_w <= 80 ? 80 : band_w <= 96 ? 96 : 128; }
+
+template <bool TAIL, int NDB, int NB>
+int launch_vert(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec* pl, NccArgs& a, const WtaOut& wo,
+                int bw, int tmax) {
+  const int bwt = vert_bw(bw, TAIL);  // (the tail kernels: one pitch)
+  if (TAIL || bwt == 128) return launch_mfma_bw<128, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);
+  return bwt == 80 ? launch_mfma_bw<80, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax)
+                   : launch_mfma_bw<96, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);
+}
+
 }  // namespace
 
-// the matrix-core form's plan: one NccMRec per (32-level chunk, neighbour)
-NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, int TH) {
-  constexpr int DC = 32, RW = sizeof(NccMRec) / 4;
+// the matrix-core form's plan: one NccMRec per (chunk of 16 ndb levels, neighbour)
+NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl, int ndb) {
+  constexpr int TH = 8, R = 2, NR = TH + 2 * R, RW = sizeof(NccMRec) / 4;
+  const int DC = 16 * ndb;
   const int nch = (D + DC - 1) / DC;
   NccPlanM p;
+  p.ndb = ndb;
   p.table.assign((size_t)nch * nn * RW, 0);
   int spx = 0;
+  // k_ncc_volume's shifts (make_plan in ncc.hip)
   auto tx_of = [&](int dl, int n) { return (int)roundf(levels[dl] * fdx[n]); };
+  auto ty_of = [&](int dl, int n) { return (int)roundf((bl * levels[dl]) * fdy[n]); };
+  for (int n = 0; n < nn; n++)
+    if (fdy[n] != 0.0f) p.vert = true;
   for (int c = 0; c < nch; c++)
     for (int n = 0; n < nn; n++) {
-      int txmin = 1 << 30, txmax = -(1 << 30);
+      int txmin = 1 << 30, txmax = -(1 << 30), tymin = 1 << 30, tymax = -(1 << 30);
       for (int dl = c * DC; dl < std::min(D, c * DC + DC); dl++) {
         txmin = std::min(txmin, tx_of(dl, n));
         txmax = std::max(txmax, tx_of(dl, n));
+        tymin = std::min(tymin, ty_of(dl, n));
+        tymax = std::max(tymax, ty_of(dl, n));
       }
+      const int par = tymax & 1;  // the bands' first row (y0 - R - tymax, y0 - tymax) is o_j's parity off a pair
+      const int bhp = (par + NR + tymax - tymin + 1) >> 1, shp = (par + TH + tymax - tymin + 1) >> 1;
       int32_t* e = p.table.data() + ((size_t)c * nn + n) * RW;
       e[0] = txmax;
-      e[1] = 0;
-      e[2] = (TH + 4) / 2;                          // pk pair rows: y0-2 .. y0+TH+1 (K = 5, no vertical shift)
-      e[3] = (TH / 2) | ((txmax - txmin) << 16);  // stats pair rows y0 .. y0+TH-1 | the chunk's column span
+      e[1] = tymax;
+      e[2] = bhp;                                  // pk pair rows: every level's y0-2 .. y0+TH+1 shifted
+      e[3] = shp | ((txmax - txmin) << 16);       // stats pair rows | the chunk's column span
       int16_t* co = (int16_t*)(e + 4);
       for (int j = 0; j < DC; j++) {
         const int dl = c * DC + j;
-        co[j] = (int16_t)(dl < D ? txmax - tx_of(dl, n) : 0);  // dummy level past the end: in-band
+        // a dummy level past the end: the band origin (in-band)
+        co[j] = (int16_t)(dl < D ? (txmax - tx_of(dl, n)) | ((par + tymax - ty_of(dl, n)) << 8) : par << 8);
       }
       spx = std::max(spx, txmax - txmin);
+      p.pk_pairs = std::max(p.pk_pairs, bhp);
+      p.st_pairs = std::max(p.st_pairs, shp);
     }
   p.band_w = 64 + spx;
   return p;
 }
 
-
-int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
-                    const WtaOut& wo, int bw, int tmax) {
-  const NccMRec* pl = (const NccMRec*)plan_dev;
-  const bool tail = a.D % 32 != 0;
-  if (mfma_tile_rows() == 8) {
-    if (tail) return launch_mfma_bw<192, 8, true>(ctx, stats, pk, pl, a, wo, tmax);
-    return bw <= 128 ? launch_mfma_bw<128, 8, false>(ctx, stats, pk, pl, a, wo, tmax)
-                     : launch_mfma_bw<192, 8, false>(ctx, stats, pk, pl, a, wo, tmax);
-  }
-  if (tail)
-    return bw <= 64    ? launch_mfma_bw<64, 4, true>(ctx, stats, pk, pl, a, wo, tmax)
-           : bw <= 128 ? launch_mfma_bw<128, 4, true>(ctx, stats, pk, pl, a, wo, tmax)
-                       : launch_mfma_bw<192, 4, true>(ctx, stats, pk, pl, a, wo, tmax);
-  return bw <= 64    ? launch_mfma_bw<64, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
-         : bw <= 80  ? launch_mfma_bw<80, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
-         : bw <= 96  ? launch_mfma_bw<96, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
-         : bw <= 128 ? launch_mfma_bw<128, 4, false>(ctx, stats, pk, pl, a, wo, tmax)
-                     : launch_mfma_bw<192, 4, false>(ctx, stats, pk, pl, a, wo, tmax);
+size_t mfma_lds_bytes(const NccPlanM& p, int band_w, int nb, int tmax, int D) {
+  const int bwt = vert_bw(band_w, D % (16 * p.ndb) != 0);
+  return std::max((size_t)nb * 16 * (p.pk_pairs + p.st_pairs) * (bwt + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
+         2 * 64 * 8 * 4 + (size_t)tmax * 16 * p.ndb * 2;
 }
 
-int mfma_tile_rows() {
-  const char* e = getenv("MVS_NCC_MFMA_TH");  // read per call (A/B): 4 or 8 (default)
-  return e && atoi(e) == 4 ? 4 : 8;
+int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
+                    const WtaOut& wo, int bw, int tmax, bool vert, int ndb, int nb) {
+  const NccMRec* pl = (const NccMRec*)plan_dev;
+  const bool tail = a.D % (16 * ndb) != 0;
+  if (vert) {
+    if (ndb == 2 && nb == 2)
+      return tail ? launch_vert<true, 2, 2>(ctx, stats, pk, pl, a, wo, bw, tmax)
+                  : launch_vert<false, 2, 2>(ctx, stats, pk, pl, a, wo, bw, tmax);
+    if (ndb == 2)
+      return tail ? launch_vert<true, 2, 1>(ctx, stats, pk, pl, a, wo, bw, tmax)
+                  : launch_vert<false, 2, 1>(ctx, stats, pk, pl, a, wo, bw, tmax);
+    if (nb == 2)
+      return tail ? launch_vert<true, 1, 2>(ctx, stats, pk, pl, a, wo, bw, tmax)
+                  : launch_vert<false, 1, 2>(ctx, stats, pk, pl, a, wo, bw, tmax);
+    return tail ? launch_vert<true, 1, 1>(ctx, stats, pk, pl, a, wo, bw, tmax)
+                : launch_vert<false, 1, 1>(ctx, stats, pk, pl, a, wo, bw, tmax);
+  }
+  if (tail) return launch_mfma_bw<192, true, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
+  return bw <= 128 ? launch_mfma_bw<128, false, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax)
+                   : launch_mfma_bw<192, false, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
 }
 
 }  // namespace ncc

@@ -153,6 +153,45 @@ def test_c4_geometry(eng, bl, nb, monkeypatch):
         assert {v[4] for v in variants} == {2}, f"MVS_NCC_NB=2 must keep double buffers, saw {sorted(variants)}"
 
 
+@pytest.mark.parametrize("form", ["auto", "22", "21", "12", "11"])
+@pytest.mark.parametrize("bl,dmax,H", [(1.0, 127, 72), (1.0359, 99, 69)])
+def test_mfma_vertical_forms(eng, form, bl, dmax, H, monkeypatch):
+    """The matrix-core fused sweep for lists with vertical / diagonal
+    neighbours (k_ncc_mfma<..., VERT>: C4's 8x4 array, 5 nearest neighbours),
+    every view of the array, each (16-level blocks per chunk, band buffers)
+    form forced through MVS_NCC_MFMA_V ("auto", MVS_NCC_MFMA_V=1: the
+    launcher's choice under two workgroups per CU; unset: the scalar kernels).  D = 128 (whole chunks) and D = 100 (dummy levels
+    in the last chunk); bl = 1.0359: fractional vertical shifts, so a chunk's
+    levels start on odd and even band rows; H = 69: an odd height (the dummy
+    row of the pair planes) and a partial last tile row."""
+    monkeypatch.setenv("MVS_NCC_MFMA_V", "1" if form == "auto" else form)
+    aw, ah, W = 8, 4, 200
+    stack, _ = synth.make_stack(W, H, aw, ah, 0, dmax, bl, 0x5EED + 6)
+    cam = _array(aw, ah, 0, dmax, knn=5, bl=bl)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    l8h = l8.cpu().numpy()
+    box = eng.box_stats(l8, 5)
+    forms = []
+    for z in range(aw * ah):
+        want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, bl, 5, z)
+        od, oc = orc.wta(want, cam.levels)
+        fd, fc = eng.ncc_wta(l8, box, cam, z, 5)
+        v = eng.ncc_last_variant()
+        same(fd, od, f"fused disp z{z} form {form}")
+        same(fc, oc, f"fused conf z{z} form {form}")
+        if v["DPW"] >= 16:  # the matrix-core form ran
+            assert v["PAR"] == 0 and v["FUSE"] == 1, v
+            forms.append(f"{v['DPW'] // 16}{v['NB']}")
+    # the corner views' lists hold a neighbour two rows away: their bands may
+    # miss the LDS cap (80 KB auto, 160 KB forced) and take the scalar kernel
+    # (at D = 100 the tail kernels' 128-column pitch: the 32-level
+    # double-buffered bands miss 160 KB for every list)
+    if form == "auto" or form != "22" or dmax == 127:
+        assert len(forms) >= aw * ah - 4, forms
+    if form != "auto":
+        assert set(forms) <= {form}, forms
+
+
 _VARIANTS = [(8, 4), (8, 2), (4, 4), (4, 2), (4, 1)]  # (waves, levels per wave): every instantiation
 _BANDS = (64, 80, 96, 128, 192, 256)  # band pitch templates (columns per pair row)
 

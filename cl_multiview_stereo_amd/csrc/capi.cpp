@@ -251,11 +251,15 @@ int mvs_slic_d(mvs_ctx* c, float* lab, int V, int W, int H, const mvs_slic_param
     }
   } else {
     uint16_t* lb16 = l16 ? (uint16_t*)scr : nullptr;
-    RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels, lb16));
+    // with the 16-bit copies, an assignment an update follows writes only them
+    // (the updates read nothing else); the last one writes the 32-bit labels
+    RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, lb16 ? nullptr : labels,
+                          lb16));
     for (int i = 0; i < p->no_iter; i++) {
       RC(mvs::launch_update(s, lab, labels, V, W, H, S, spixl, part, lb16));
-      RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels,
-                            i + 1 < p->no_iter ? lb16 : nullptr));
+      const bool more = i + 1 < p->no_iter;
+      RC(mvs::launch_assign(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search,
+                            more && lb16 ? nullptr : labels, more ? lb16 : nullptr));
     }
   }
   if (p->enforce_connectivity) {

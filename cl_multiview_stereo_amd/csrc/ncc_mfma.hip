@@ -66,7 +66,9 @@ constexpr int kMfMergeStride = 257;  // LDS merge rows: 256 pixels + 1 (16 class
 // end.  NDB: 16-level blocks per chunk (DC = 16 NDB levels per step).  NB:
 // band buffers (2: step t+1's bands land while step t computes; 1: staged at
 // the start of each step, the other resident workgroup computing meanwhile).
-template <int BW, bool TAIL, bool VERT, int NDB, int NB>
+// DBG (timing probe only, MVS_NCC_MFMA_DBG): 1 skips the MFMAs and the
+// finish (band DMA, barriers, fold and merge stay), 2 skips the band DMA
+template <int BW, bool TAIL, bool VERT, int NDB, int NB, int DBG = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_mfma(
     const uint2* __restrict__ stats, const uint2* __restrict__ pk, const NccMRec* __restrict__ plan, NccArgs a,
     WtaOut wo) {
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   const long pk_row = 2L * W * min(max((y0 - R) / 2 + wave, 0), Hp2 - 1);  // (y0 - R) even: y0 even, R = 2
   const long st_row = 2L * W * min(max(y0 / 2 + wave, 0), Hp2 - 1);
   auto stage = [&](int t, int n, int b) {
+    if (DBG == 2) return;
     const NccMRec& e = rec[t];
     const int span = e.shp >> 16, nblk = (span + 127) >> 6;
     const long vo = (long)a.view[ref][n] * Pv;
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     };
     // one level block at a time (at the 128-VGPR cap the paired form spilled 16-40 B)
 #pragma unroll
-    for (int k = 0; k < 2 * NYB; k++) {
+    for (int k = 0; k < (DBG == 1 ? 0 : 2 * NYB); k++) {
       const int xb = k / NYB, yb = k % NYB;
       const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
 #pragma unroll
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
-template <int BW, bool TAIL, bool VERT, int NDB, int NB>
+template <int BW, bool TAIL, bool VERT, int NDB, int NB, int DBG = 0>
 int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec* plan, NccArgs& a,
                    const WtaOut& wo, int tmax) {
   constexpr int TH = 8, DC = 16 * NDB;
@@ -443,7 +446,7 @@ int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccM
   a.nch = (a.D + DC - 1) / DC;
   const size_t lds = std::max((size_t)NB * 16 * (a.pk_pairs + a.st_pairs) * (BW + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
                      2 * 64 * TH * 4 + (size_t)tmax * DC * 2;
-  auto kern = k_ncc_mfma<BW, TAIL, VERT, NDB, NB>;
+  auto kern = k_ncc_mfma<BW, TAIL, VERT, NDB, NB, DBG>;
   static size_t lds_set = 64 * 1024;  // per instantiation: raise the limit once, not on every launch
   if (lds > lds_set) {
     MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -462,6 +465,12 @@ template <bool TAIL, int NDB, int NB>
 int launch_vert(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec* pl, NccArgs& a, const WtaOut& wo,
                 int bw, int tmax) {
   const int bwt = vert_bw(bw, TAIL);  // (the tail kernels: one pitch)
+  if (!TAIL && NDB == 1 && NB == 2 && bwt == 80) {  // timing probe (C4's interior lists): MVS_NCC_MFMA_DBG=1 | 2
+    const char* dbg = getenv("MVS_NCC_MFMA_DBG");
+    const int dv = dbg ? atoi(dbg) : 0;
+    if (dv == 1) return launch_mfma_bw<80, false, true, 1, 2, 1>(ctx, stats, pk, pl, a, wo, tmax);
+    if (dv == 2) return launch_mfma_bw<80, false, true, 1, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
+  }
   if (TAIL || bwt == 128) return launch_mfma_bw<128, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);
   return bwt == 80 ? launch_mfma_bw<80, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax)
                    : launch_mfma_bw<96, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);

@@ -310,8 +310,8 @@ __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, 
         min_id = take ? (float)(cy * mw + cx) : min_id;
         have = have || take;
       }
-    labels[pid] = (uint32_t)min_id;
-    if (lb16) lb16[pid] = (uint16_t)min_id;  // the next k_update's 16-bit copy (mw * mh <= 65536)
+    if (labels) labels[pid] = (uint32_t)min_id;  // (null: an update follows, reading only the copy)
+    if (lb16) lb16[pid] = (uint16_t)min_id;      // the next k_update's 16-bit copy (mw * mh <= 65536)
   }
 }
 
@@ -486,6 +486,137 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
       o[3] = acc[2] * r;
       o[4] = acc[3] * r;
       o[5] = acc[4] * r;
+      o[6] = n;
+    } else {
+      o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
+    }
+  }
+}
+
+// k_update's window walk with the per-tile work cut to what the window
+// needs (C5, S = 40: k_update<4, uint16_t> executed ~131 VALU and ~72 SALU
+// per window tile, 296 M + 162 M per launch, VALU-issue-bound at 568 us):
+//  * the tile coordinates advance incrementally (t % cpl, t / cpl were SALU
+//    division sequences), and every address is a 32-bit buffer offset: the
+//    tile origin (scalar) plus the lane's fixed offset, one add per load and
+//    no select -- the view's buffer resource bounds it, and a pixel outside
+//    the window or the image is dropped by its in-test as before;
+//  * a pixel is tested with three compares (column: once per tile; the row
+//    against the window and the image; the label);
+//  * the colours are gathered only for tiles holding a member (uniform
+//    branch), unconditionally inside them (non-members select an exact 0);
+//  * the three colour trees run together (wave_tree4s: each channel's
+//    additions are wave_tree's, in its order), accumulated in their result
+//    lanes (0: L, 32: a, 16: b), x / y / count as k_update's integer tree.
+// Bit-identical to k_update (the same per-tile trees, the same tile order).
+typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+template <int UT, typename LT>
+__global__ __launch_bounds__(256) void k_update_walk(const float4* __restrict__ lab, const LT* __restrict__ labels,
+                                                     int W, int H, int S, int mw, int mh, int G, int cpl,
+                                                     float* __restrict__ spixl) {
+  const int lane = threadIdx.x & 63;
+  const int sp = blockIdx.x * 4 + (threadIdx.x >> 6), z = blockIdx.y;
+  if (sp >= mw * mh) return;  // whole wave; no barriers
+  const int gx = sp % mw, gy = sp / mw;
+  const long P = (long)W * H;
+  // the launcher checks P * 16 < 2^31
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(labels + z * P), 0, (int)(P * sizeof(LT)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)(lab + z * P), 0, (int)(P * 16), 0x00020000);
+  const int lx = lane & 15, ly0 = lane >> 4, S3 = 3 * S;
+  const int x0 = gx * S - S, y0 = gy * S - S;  // the window's origin
+  const int loff = ly0 * W + lx;                // the lane's pixel offset in a tile (row m: + 4 m W)
+  const unsigned loffl = (unsigned)loff * (unsigned)sizeof(LT), loffc = (unsigned)loff * 16u;  // in bytes
+  const uint32_t lpk = (uint32_t)lx | (uint32_t)ly0 << 12 | 1u << 24;
+  float acc3 = 0.0f;                        // colour partial sums: lane 0 L, 32 a, 16 b
+  float accx = 0.0f, accy = 0.0f, accn = 0.0f;  // lane 0
+  int nbx = 0, nby = 0;                     // window tile of t0
+  for (int t0 = 0; t0 < G; t0 += UT) {
+    LT lb[UT][4];
+    int tb[UT], bxs[UT], bys[UT], nys[UT];
+    bool inx[UT];
+#pragma unroll
+    for (int u = 0; u < UT; u++) {
+      bxs[u] = x0 + nbx * kLocal;
+      bys[u] = y0 + nby * kLocal;
+      nys[u] = nby * kLocal;
+      tb[u] = bys[u] * W + bxs[u];  // tile origin's pixel offset (may be negative: dropped lanes)
+      inx[u] = t0 + u < G && (unsigned)(bxs[u] + lx) < (unsigned)W && nbx * kLocal + lx < S3;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        // scalar tile-row offset + the lane's pre-scaled offset: one add per load
+        const unsigned o = (unsigned)(tb[u] + 4 * m * W) * (unsigned)sizeof(LT) + loffl;
+        if (sizeof(LT) == 2)
+          lb[u][m] = (LT)__builtin_amdgcn_raw_buffer_load_b16(rl, (int)o, 0, 0);
+        else
+          lb[u][m] = (LT)__builtin_amdgcn_raw_buffer_load_b32(rl, (int)o, 0, 0);
+      }
+      if (++nbx == cpl) {
+        nbx = 0;
+        nby++;
+      }
+    }
+    bool mem[UT][4], anyt[UT];
+#pragma unroll
+    for (int u = 0; u < UT; u++) {
+      bool any = false;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const int py = bys[u] + ly0 + 4 * m;
+        mem[u][m] = inx[u] && nys[u] + ly0 + 4 * m < S3 && (unsigned)py < (unsigned)H && lb[u][m] == (LT)sp;
+        any |= mem[u][m];
+      }
+      anyt[u] = __any(any);
+    }
+    u32x3 c[UT][4];
+#pragma unroll
+    for (int u = 0; u < UT; u++)
+      if (anyt[u])
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+          c[u][m] = __builtin_amdgcn_raw_buffer_load_b96(rc, (int)((unsigned)(tb[u] + 4 * m * W) * 16u + loffc), 0, 0);
+#pragma unroll
+    for (int u = 0; u < UT; u++) {
+      if (t0 + u >= G) break;
+      float rx = 0.0f, ry = 0.0f, rn = 0.0f, r3 = 0.0f;
+      if (anyt[u]) {
+        uint32_t pk[4];
+        float v[3][4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+          pk[m] = mem[u][m] ? lpk + ((uint32_t)(4 * m) << 12) : 0u;
+          v[0][m] = mem[u][m] ? __uint_as_float(c[u][m].x) : 0.0f;
+          v[1][m] = mem[u][m] ? __uint_as_float(c[u][m].y) : 0.0f;
+          v[2][m] = mem[u][m] ? __uint_as_float(c[u][m].z) : 0.0f;
+        }
+        const uint32_t q = wave_sum_u32(pk[0], pk[1], pk[2], pk[3]);
+        const int cnt = (q >> 24) ? (int)(q >> 24) : 256;
+        rx = (float)((int)(q & 0xfffu) + cnt * bxs[u]);  // the sum of member x: exact below 2^24
+        ry = (float)((int)((q >> 12) & 0xfffu) + cnt * bys[u]);
+        rn = (float)cnt;
+        float sc[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) sc[ch] = (v[ch][0] + v[ch][2]) + (v[ch][1] + v[ch][3]);
+        r3 = wave_tree4s(sc[0], sc[1], sc[2], 0.0f);  // lanes 0: L, 32: a, 16: b
+      }
+      accx = accx + rx;
+      accy = accy + ry;
+      acc3 = acc3 + r3;
+      accn = accn + rn;
+    }
+  }
+  const float aL = __shfl(acc3, 0), aa = __shfl(acc3, 32), ab = __shfl(acc3, 16);
+  if (lane == 0) {
+    float* o = spixl + 8 * ((long)z * mw * mh + sp);
+    const float n = accn;
+    o[0] = (float)sp;
+    if (n != 0) {
+      const float r = 1.0f / n;  // x * RN(1/n), as k_update
+      o[1] = accx * r;
+      o[2] = accy * r;
+      o[3] = aL * r;
+      o[4] = aa * r;
+      o[5] = ab * r;
       o[6] = n;
     } else {
       o[1] = o[2] = o[3] = o[4] = o[5] = o[6] = 0.0f;
@@ -1049,6 +1180,7 @@ int launch_grid_labels(hipStream_t s, int V, int W, int H, int S, uint32_t* labe
 int launch_assign(hipStream_t s, const float* lab, const float* spixl, int V, int W, int H, int S, float xy_n,
                   float col_n, float weight, int search, uint32_t* labels, uint16_t* lb16) {
   int mw = map_dim(W, S), mh = map_dim(H, S);
+  if (!labels && !(lb16 && (long)mw * mh <= 65536)) return arg_fail("SLIC assign: no label output");
   if ((AS_TW / S + 4) * (AS_TH / S + 4) > AS_MAXC) return arg_fail("SLIC assign: spixl_size too small");
   hipLaunchKernelGGL(search ? k_assign<true> : k_assign<false>, dim3((W + AS_TW - 1) / AS_TW, (H + AS_TH - 1) / AS_TH, V), dim3(256), 0, s,
                      (const float4*)lab, spixl, W, H, S, mw, mh, xy_n, col_n, weight, labels,
@@ -1107,6 +1239,23 @@ int launch_update(hipStream_t s, const float* lab, const uint32_t* labels, int V
     hipLaunchKernelGGL(cpl == 6 ? k_update_finalize<6> : k_update_finalize<0>, dim3((mw * mh + 31) / 32, V),
                        dim3(256), 0, s, part, mw, mh, S, G, cpl, ntx, nty, spixl);
     MVS_LAUNCH_CHECK("k_update_finalize");
+    return 0;
+  }
+  // k_update_walk (32-bit buffer offsets: P * 16 < 2^31); MVS_SLIC_UPDATE=0
+  // (read per call): k_update (A/B)
+  const char* ue = getenv("MVS_SLIC_UPDATE");
+  const bool walk = (long)W * H * 16 < (1L << 31) && !(ue && atoi(ue) == 0);
+  if (walk) {
+    const bool l16 = lb16 && (long)mw * mh <= 65536;
+    const dim3 g((mw * mh + 3) / 4, V);
+    if (l16) {
+      auto kw = G > 4 ? k_update_walk<4, uint16_t> : k_update_walk<1, uint16_t>;
+      hipLaunchKernelGGL(kw, g, dim3(256), 0, s, (const float4*)lab, lb16, W, H, S, mw, mh, G, cpl, spixl);
+    } else {
+      auto kw = G > 4 ? k_update_walk<4, uint32_t> : k_update_walk<1, uint32_t>;
+      hipLaunchKernelGGL(kw, g, dim3(256), 0, s, (const float4*)lab, labels, W, H, S, mw, mh, G, cpl, spixl);
+    }
+    MVS_LAUNCH_CHECK("k_update_walk");
     return 0;
   }
   if (lb16 && (long)mw * mh <= 65536) {  // the 16-bit copy the previous launch_assign wrote

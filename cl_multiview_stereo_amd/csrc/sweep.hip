@@ -109,8 +109,37 @@ struct SweepArgs {
 // TL = false (no re-laid views in this call, e.g. a horizontal array): the
 // row-major addressing folds to yp W + xp at compile time -- the general
 // form's extra multiply-add per tap cost C2 (5x1 array) 173 -> 224 us.
+// HZ (every neighbour of the launch's references in the same camera row, every
+// level x column offset an integer below 2^24, no re-laid views): the shift
+// is an integer, so (int)((float)xr - d dx) = xr - (int)(d dx) exactly, the
+// tap's row yr = (int)(r.y - 0) is the reference tap's own (inside the image
+// whenever the reference tap is) and its offset yr W is stored with the tap.
+// A tap then costs one integer subtract, one compare and one shift-add before
+// its gather, and the gather needs no select: the view's buffer resource
+// bounds every offset (a tap outside the image reads some pixel of the view,
+// or 0, and is dropped as before).  The absolute differences and the
+// reference's val += 30; val -= 30; val += AD are single-issue asm, as the
+// compiler's SLP pairing put them in v_pk_add_f32 with the |.| as separate
+// v_and_b32.  C2: see DESIGN.md section 3.
 typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
-template <int LPS, bool TL>
+__device__ __forceinline__ float tap_ad(const float4& A, const u32x3& bv) {
+  float t0, t1, t2, r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(t0) : "v"(A.x), "v"(__uint_as_float(bv.x)));
+  asm("v_sub_f32 %0, %1, %2" : "=v"(t1) : "v"(A.y), "v"(__uint_as_float(bv.y)));
+  asm("v_add_f32 %0, |%1|, |%2|" : "=v"(r) : "v"(t0), "v"(t1));  // fabsf(dL) + fabsf(da)
+  asm("v_sub_f32 %0, %1, %2" : "=v"(t2) : "v"(A.z), "v"(__uint_as_float(bv.z)));
+  asm("v_add_f32 %0, %1, |%2|" : "=v"(r) : "v"(r), "v"(t2));  // + fabsf(db)
+  return r;
+}
+// val = in ? ((val + 30) - 30) + ad : val + 30
+__device__ __forceinline__ float tap_acc(float val, float ad, bool in) {
+  float v30, t;
+  asm("v_add_f32 %0, 0x41f00000, %1" : "=v"(v30) : "v"(val));
+  asm("v_add_f32 %0, 0xc1f00000, %1" : "=v"(t) : "v"(v30));
+  asm("v_add_f32 %0, %1, %2" : "=v"(t) : "v"(t), "v"(ad));
+  return in ? t : v30;
+}
+template <int LPS, bool TL, bool HZ = false>
 __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ lab, float* __restrict__ spixl,
                                                      const uint8_t* __restrict__ rep,
                                                      const float* __restrict__ levels, const int* __restrict__ vs,
@@ -119,6 +148,7 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
                                                      const int* __restrict__ tslot, long tstride) {
   __shared__ float4 refc[8][25];
   __shared__ float2 refxy[8][25];  // (float)xr, (float)yr; xr = -1e9 for a tap outside the image
+                                   // (HZ: int xr (-2^30 outside), int yr W)
   __shared__ float wbest[4];
   __shared__ int wbi[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -150,7 +180,10 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
     int yr = (int)(cy + (float)j * sty);
     bool in = xr >= 0 && yr >= 0 && xr < a.W && yr < a.H;
     // (float)xr is exact; an outside reference tap projects outside too
-    refxy[slot][ll] = make_float2(in ? (float)xr : -1.0e9f, (float)yr);
+    if (HZ)
+      refxy[slot][ll] = make_float2(__int_as_float(in ? xr : -(1 << 30)), __int_as_float(in ? yr * a.W : 0));
+    else
+      refxy[slot][ll] = make_float2(in ? (float)xr : -1.0e9f, (float)yr);
     refc[slot][ll] = in ? labz[(long)yr * a.W + xr] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
@@ -167,6 +200,23 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
       float fdx = d * (float)(vx - rx);
       float fdy = (a.bl * d) * (float)(vy - ry);
       const int ddx = vx - rx, ddy = vy - ry;
+      if (HZ) {
+        const int sh = (int)fdx;  // exact (the launcher checked the levels)
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(lab + (long)view * P), 0, (int)(P * 16), 0x00020000);
+        float val = 0.0f;
+#pragma unroll 5
+        for (int t = 0; t < 25; t++) {
+          const float2 rf = refxy[slot][t];
+          const int xp = __float_as_int(rf.x) - sh;
+          const bool in = (unsigned)xp < (unsigned)a.W;
+          const unsigned bo = (unsigned)(__float_as_int(rf.y) + xp) << 4;
+          const u32x3 bv = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)bo, 0, 0);
+          val = tap_acc(val, tap_ad(refc[slot][t], bv), in);
+        }
+        if (val < mn) mn = val;
+        continue;
+      }
       const int kind = !TL ? 0 : ddx == 0 ? 1 : ddx == ddy ? 2 : ddx == -ddy ? 3 : 0;
       const int ts = TL && kind ? tslot[4 * view + kind] : -1;
       const float4* labv = TL && ts >= 0 ? labT + (long)ts * tstride : lab + (long)view * P;
@@ -187,14 +237,12 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
         const int xp = (int)(r.x - fdx);
         const int yp = (int)(r.y - fdy);
         const bool in = (unsigned)xp < (unsigned)a.W && (unsigned)yp < (unsigned)a.H;
-        const int bo = in ? (off + yp * sys + xp * sxs) * 16 : 0;  // an outside tap reads pixel 0, dropped below
+        // 24-bit multiplies (full rate; the 32-bit v_mul_lo_u32 is quarter
+        // rate): an inside tap's |yp|, |xp| < 2^23 and |sys|, sxs <= W + H
+        const int bo = in ? (off + __mul24(yp, sys) + __mul24(xp, sxs)) * 16 : 0;  // an outside tap reads pixel 0, dropped below
         const u32x3 bv = __builtin_amdgcn_raw_buffer_load_b96(rs, bo, 0, 0);
-        const float3 B = make_float3(__uint_as_float(bv.x), __uint_as_float(bv.y), __uint_as_float(bv.z));
-        const float4 A = refc[slot][t];
-        float ad = fabsf(A.x - B.x) + fabsf(A.y - B.y);
-        ad = ad + fabsf(A.z - B.z);
-        const float v30 = val + 30.0f;  // the reference's val += 30; val -= 30; val += AD
-        val = in ? (v30 - 30.0f) + ad : v30;
+        // the reference's fabs sums and val += 30; val -= 30; val += AD
+        val = tap_acc(val, tap_ad(refc[slot][t], bv), in);
       }
       if (val < mn) mn = val;
     }
@@ -766,7 +814,8 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
   if (z1 <= z0) return 0;
   // k_sweep_spixl's 32-bit byte offsets within a view (a re-laid one spans
   // at most (W + H) H elements)
-  if ((long)(W + H) * H * 16 >= (1L << 31)) return arg_fail("superpixel sweep: image too large for 32-bit offsets");
+  if ((long)(W + H) * H * 16 >= (1L << 31) || W >= (1 << 23) || H >= (1 << 23))  // (+ its 24-bit multiplies)
+    return arg_fail("superpixel sweep: image too large for 32-bit offsets");
   hipStream_t s = ctx->stream;
   int mw = map_dim(W, S), mh = map_dim(H, S);
   long M = (long)mw * mh;
@@ -829,7 +878,22 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
       if (units > 0) labT = buf;
     }
   }
+  // HZ: every neighbour of [z0, z1) in the reference's camera row and every
+  // level x column offset an integer of magnitude below 2^24 (MVS_SWEEP_HZ=0,
+  // read per call: the general form, A/B)
+  bool hz = !labT && (long)W * H * 16 < (1L << 31) && !(getenv("MVS_SWEEP_HZ") && atoi(getenv("MVS_SWEEP_HZ")) == 0);
+  for (int z = z0; z < z1 && hz; z++)
+    for (int k = 0; k < ctx->h_sn[z] && hz; k++) {
+      const int v = ctx->h_vs[(size_t)V * z + k];
+      if (v / aw != z / aw) hz = false;
+      const float fdxv = (float)(v % aw - z % aw);
+      for (int l = 0; l < D && hz; l++) {
+        const float f = ctx->h_levels[l] * fdxv;  // the kernel's d * (float)(vx - rx)
+        if (!(fabsf(f) < 16777216.0f) || f != truncf(f)) hz = false;
+      }
+    }
   auto kern = labT ? (half ? k_sweep_spixl<32, true> : k_sweep_spixl<64, true>)
+              : hz ? (half ? k_sweep_spixl<32, false, true> : k_sweep_spixl<64, false, true>)
                    : (half ? k_sweep_spixl<32, false> : k_sweep_spixl<64, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * ((nb + 7) / 8)), (unsigned)(z1 - z0)), dim3(256), 0, s,
                      (const float4*)lab, spixl, rep, levels, vs, sn, a, wps, labT, tslot, tstride);

@@ -242,12 +242,14 @@ int mvs_slic_d(mvs_ctx* c, float* lab, int V, int W, int H, const mvs_slic_param
   if (part && S % 16 == 0) {
     // assign -> (update -> assign) x no_iter with each update's tile partials
     // produced by the assign pass before it (one Lab read per iteration)
-    RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels,
-                                p->no_iter > 0 ? part : nullptr));
+    // (an assignment an update follows stores no labels: the update reads its partials only)
+    RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search,
+                                p->no_iter > 0 ? nullptr : labels, p->no_iter > 0 ? part : nullptr));
     for (int i = 0; i < p->no_iter; i++) {
       RC(mvs::launch_update_finalize(s, part, V, W, H, S, spixl));
-      RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search, labels,
-                                  i + 1 < p->no_iter ? part : nullptr));
+      const bool more = i + 1 < p->no_iter;
+      RC(mvs::launch_assign_tiles(s, lab, spixl, V, W, H, S, xy, col, p->color_weight, p->search,
+                                  more ? nullptr : labels, more ? part : nullptr));
     }
   } else {
     uint16_t* lb16 = l16 ? (uint16_t*)scr : nullptr;

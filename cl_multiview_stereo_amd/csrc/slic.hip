@@ -503,8 +503,9 @@ __global__ __launch_bounds__(256) void k_update(const float4* __restrict__ lab, 
 //    the window or the image is dropped by its in-test as before;
 //  * a pixel is tested with three compares (column: once per tile; the row
 //    against the window and the image; the label);
-//  * the colours are gathered only for tiles holding a member (uniform
-//    branch), unconditionally inside them (non-members select an exact 0);
+//  * a colour is gathered for members only: a non-member's load is sent
+//    past the buffer's records (no memory access, 0 -- the exact zero the
+//    tree adds for it);
 //  * the three colour trees run together (wave_tree4s: each channel's
 //    additions are wave_tree's, in its order), accumulated in their result
 //    lanes (0: L, 32: a, 16: b), x / y / count as k_update's integer tree.
@@ -556,25 +557,24 @@ __global__ __launch_bounds__(256) void k_update_walk(const float4* __restrict__ 
         nby++;
       }
     }
+    // membership without short-circuit branches; a non-member's colour load
+    // is sent past the records (no memory access, reads 0: the exact zero the
+    // tree needs), so only members move colour bytes
     bool mem[UT][4], anyt[UT];
+    u32x3 c[UT][4];
 #pragma unroll
     for (int u = 0; u < UT; u++) {
       bool any = false;
 #pragma unroll
       for (int m = 0; m < 4; m++) {
         const int py = bys[u] + ly0 + 4 * m;
-        mem[u][m] = inx[u] && nys[u] + ly0 + 4 * m < S3 && (unsigned)py < (unsigned)H && lb[u][m] == (LT)sp;
+        mem[u][m] = inx[u] & (nys[u] + ly0 + 4 * m < S3) & ((unsigned)py < (unsigned)H) & (lb[u][m] == (LT)sp);
         any |= mem[u][m];
+        const unsigned oc = (unsigned)(tb[u] + 4 * m * W) * 16u + loffc;
+        c[u][m] = __builtin_amdgcn_raw_buffer_load_b96(rc, mem[u][m] ? (int)oc : 0x7fffffff, 0, 0);
       }
       anyt[u] = __any(any);
     }
-    u32x3 c[UT][4];
-#pragma unroll
-    for (int u = 0; u < UT; u++)
-      if (anyt[u])
-#pragma unroll
-        for (int m = 0; m < 4; m++)
-          c[u][m] = __builtin_amdgcn_raw_buffer_load_b96(rc, (int)((unsigned)(tb[u] + 4 * m * W) * 16u + loffc), 0, 0);
 #pragma unroll
     for (int u = 0; u < UT; u++) {
       if (t0 + u >= G) break;
@@ -585,9 +585,9 @@ __global__ __launch_bounds__(256) void k_update_walk(const float4* __restrict__ 
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           pk[m] = mem[u][m] ? lpk + ((uint32_t)(4 * m) << 12) : 0u;
-          v[0][m] = mem[u][m] ? __uint_as_float(c[u][m].x) : 0.0f;
-          v[1][m] = mem[u][m] ? __uint_as_float(c[u][m].y) : 0.0f;
-          v[2][m] = mem[u][m] ? __uint_as_float(c[u][m].z) : 0.0f;
+          v[0][m] = __uint_as_float(c[u][m].x);  // (0 for a non-member: its load read nothing)
+          v[1][m] = __uint_as_float(c[u][m].y);
+          v[2][m] = __uint_as_float(c[u][m].z);
         }
         const uint32_t q = wave_sum_u32(pk[0], pk[1], pk[2], pk[3]);
         const int cnt = (q >> 24) ? (int)(q >> 24) : 256;
@@ -771,7 +771,7 @@ __global__ __launch_bounds__(256) void k_assign_tiles(const float4* __restrict__
         have = have || take;
       }
     lbl[m] = (uint32_t)min_id;
-    labels[(long)z * P + (long)row * W + col] = lbl[m];
+    if (labels) labels[(long)z * P + (long)row * W + col] = lbl[m];  // (null: an update follows)
   }
   if (!part) return;
   float* out = part + (long)z * mw * mh * G * 6;
@@ -894,8 +894,9 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
   float cid[4];  // the candidates' labels as k_assign forms them
 #pragma unroll
   for (int i = 0; i < 4; i++) cid[i] = (float)(ccy[i] * mw + ccx[i]);
-  const __amdgpu_buffer_rsrc_t rlb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(labels + (long)z * P), 0, (int)(P * 4), 0x00020000);
+  // labels null (an update follows: its partials are all it reads): no records, every store dropped
+  const __amdgpu_buffer_rsrc_t rlb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(labels ? labels + (long)z * P : nullptr), 0, labels ? (int)(P * 4) : 0, 0x00020000);
   uint32_t lbl[4];
   int win[4];  // the pixel's candidate (-1: none, or outside the image)
 #pragma unroll

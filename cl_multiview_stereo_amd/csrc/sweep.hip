@@ -82,6 +82,13 @@ __global__ __launch_bounds__(256) void k_boundary(const float* __restrict__ spix
   if (lane == 0) *(uint2*)(rep + 8 * (z * M + s)) = make_uint2(w, hi);
 }
 
+// 16-byte LDS-DMA: lane l's 16 bytes land at dst + 16 l (dst wave-uniform)
+typedef __attribute__((address_space(3))) void* lds_vptr_t;
+typedef const __attribute__((address_space(1))) void* glb_vptr_t;
+__device__ __forceinline__ void glds16(const void* src, void* dst) {
+  __builtin_amdgcn_global_load_lds((glb_vptr_t)src, (lds_vptr_t)dst, 16, 0, 0);
+}
+
 // ---- initial_depth_estimation_v2, clcode.cl:972-1069 ----------------------
 struct SweepArgs {
   int V, W, H, mw, mh, D, aw, z;
@@ -122,6 +129,7 @@ struct SweepArgs {
 // compiler's SLP pairing put them in v_pk_add_f32 with the |.| as separate
 // v_and_b32.  C2: see DESIGN.md section 3.
 typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float tap_ad(const float4& A, const u32x3& bv) {
   float t0, t1, t2, r;
   asm("v_sub_f32 %0, %1, %2" : "=v"(t0) : "v"(A.x), "v"(__uint_as_float(bv.x)));
@@ -237,12 +245,14 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
         const int xp = (int)(r.x - fdx);
         const int yp = (int)(r.y - fdy);
         const bool in = (unsigned)xp < (unsigned)a.W && (unsigned)yp < (unsigned)a.H;
-        // 24-bit multiplies (full rate; the 32-bit v_mul_lo_u32 is quarter
-        // rate): an inside tap's |yp|, |xp| < 2^23 and |sys|, sxs <= W + H
-        const int bo = in ? (off + __mul24(yp, sys) + __mul24(xp, sxs)) * 16 : 0;  // an outside tap reads pixel 0, dropped below
+        const int bo = in ? (off + yp * sys + xp * sxs) * 16 : 0;  // an outside tap reads pixel 0, dropped below
         const u32x3 bv = __builtin_amdgcn_raw_buffer_load_b96(rs, bo, 0, 0);
-        // the reference's fabs sums and val += 30; val -= 30; val += AD
-        val = tap_acc(val, tap_ad(refc[slot][t], bv), in);
+        const float3 B = make_float3(__uint_as_float(bv.x), __uint_as_float(bv.y), __uint_as_float(bv.z));
+        const float4 A = refc[slot][t];
+        float ad = fabsf(A.x - B.x) + fabsf(A.y - B.y);
+        ad = ad + fabsf(A.z - B.z);
+        const float v30 = val + 30.0f;  // the reference's val += 30; val -= 30; val += AD
+        val = in ? (v30 - 30.0f) + ad : v30;
       }
       if (val < mn) mn = val;
     }
@@ -272,6 +282,255 @@ __global__ __launch_bounds__(256) void k_sweep_spixl(const float4* __restrict__ 
   __syncthreads();
   if (active && h == 0 && lane == 0) {
     for (int k = 1; k < wps; k++) {
+      const float ob = wbest[w + k];
+      const int oi = wbi[w + k];
+      if (ob < best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    spixl[8 * idx + 7] = (bi != 0x7fffffff && best < 1000000.0f) ? levels[bi] : 0.0f;
+  }
+}
+
+// ---- the HZ sweep from LDS-staged rows (k_sweep_spixl_ring) ---------------
+// The HZ gather form is texture-address-bound, not VALU-bound (C2, PMC: TA
+// busy 74 % of the kernel, ~15 L2 requests per 64-lane gather: the 64 levels
+// of one tap hit 64 pixels dx apart, a partial line each, and the 5 taps of a
+// row re-read the same pixels at other levels).  Here a wave (64 levels of
+// one superpixel) stages, per neighbour and tap row, the union of the columns
+// its 5 taps reach at its 64 levels -- [min xr - max sh, max xr - min sh],
+// clamped to the image, at most kSwU columns -- into LDS by whole-line
+// LDS-DMA (one 1 KiB piece per 64 columns), and reads every tap from there.
+// Rows go through a two-slot ring per wave: row k+2 is staged while row k+1
+// lands and row k is computed (s_waitcnt vmcnt(pieces of row k+1) before
+// row k); no barrier, the ring is the wave's own.  A tap's absolute
+// differences are k_sweep_spixl's; its out-of-image flag rides as ad = -1
+// (ad >= 0 otherwise), and the reference's val += 30; val -= 30; val += AD
+// chain runs in tap order (i outer, j inner) once the neighbour's 25 taps
+// are in.  The launcher takes this form only when every window fits kSwU
+// columns: 2 (S - 1) + 2 + |dx| x the levels' range over any 64 consecutive
+// levels (stx <= (S - 1) / 2), else the HZ gathers.
+constexpr int kSwU = 336;  // C5 (S = 40, |dx| <= 4): 78 + 2 + 252 = 332
+__device__ __forceinline__ void wait_vm(int n) {  // s_waitcnt vmcnt(n), n in [0, 6]
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    case 1: __builtin_amdgcn_s_waitcnt(0x0f71); break;
+    case 2: __builtin_amdgcn_s_waitcnt(0x0f72); break;
+    case 3: __builtin_amdgcn_s_waitcnt(0x0f73); break;
+    case 4: __builtin_amdgcn_s_waitcnt(0x0f74); break;
+    case 5: __builtin_amdgcn_s_waitcnt(0x0f75); break;
+    default: __builtin_amdgcn_s_waitcnt(0x0f76); break;
+  }
+}
+__device__ __forceinline__ float wave_min_f(float v) {
+  v = fminf(v, __shfl_xor(v, 32));
+  v = fminf(v, __shfl_xor(v, 16));
+  v = fminf(v, __shfl_xor(v, 8));
+  v = fminf(v, __shfl_xor(v, 4));
+  v = fminf(v, __shfl_xor(v, 2));
+  v = fminf(v, __shfl_xor(v, 1));
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+template <int WPS>
+__global__ __launch_bounds__(256) void k_sweep_spixl_ring(const float4* __restrict__ lab, float* __restrict__ spixl,
+                                                          const uint8_t* __restrict__ rep,
+                                                          const float* __restrict__ levels, const int* __restrict__ vs,
+                                                          const int* __restrict__ sn, SweepArgs a) {
+  constexpr int SPB = 4 / WPS;
+  __shared__ __align__(16) float4 ring[4][2][kSwU];  // per wave: two row slots
+  __shared__ float4 refc[SPB][25];
+  __shared__ int rxr[SPB][5], ryr[SPB][5];           // tap columns (i) and rows (j), possibly outside
+  __shared__ unsigned rvm[SPB];                       // bit 5 i + j: tap (i, j) inside the image
+  __shared__ float wbest[4];
+  __shared__ int wbi[4];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = w % WPS, slot = w / WPS;
+  const int z = a.z + blockIdx.y;
+  const long M = (long)a.mw * a.mh, P = (long)a.W * a.H;
+  const long nbk = (M + SPB - 1) / SPB, per = (nbk + 7) / 8;  // XCD-aware order, as k_sweep_spixl
+  const long blk = (long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const long s = blk * SPB + slot;
+  const bool active = blk < nbk && s < M;
+  const long idx = z * M + (active ? s : 0);
+  if (h == 0) {
+    const uint8_t* dr = rep + 8 * idx;
+    const int bl_ = max((int)dr[0], max((int)dr[1], (int)dr[2]));
+    const int br_ = max((int)dr[5], max((int)dr[6], (int)dr[7]));
+    const int bt_ = max((int)dr[0], max((int)dr[3], (int)dr[5]));
+    const int bb_ = max((int)dr[2], max((int)dr[4], (int)dr[7]));
+    const float stx = (float)fmax(1.0, 0.25 * (double)(float)(bl_ + br_));
+    const float sty = (float)fmax(1.0, 0.25 * (double)(float)(bt_ + bb_));
+    const float cx = spixl[8 * idx + 1], cy = spixl[8 * idx + 2];
+    const int i = lane / 5 - 2, j = lane % 5 - 2;  // tap t = lane: i (x) outer, j (y) inner
+    const int xr = (int)(cx + (float)i * stx);
+    const int yr = (int)(cy + (float)j * sty);
+    const bool in = lane < 25 && xr >= 0 && yr >= 0 && xr < a.W && yr < a.H;
+    if (lane < 25) {
+      // .w: the tap's column, or -2^30 for a tap outside the image (its projection is outside too)
+      float4 rc = in ? lab[(long)z * P + (long)yr * a.W + xr] : make_float4(0.f, 0.f, 0.f, 0.f);
+      rc.w = __int_as_float(in ? xr : -(1 << 30));
+      refc[slot][lane] = rc;
+      if (j == -2) rxr[slot][i + 2] = xr;
+      if (i == -2) ryr[slot][j + 2] = yr;
+    }
+    const unsigned long long bal = __ballot(in);
+    if (lane == 0) rvm[slot] = (unsigned)bal;
+  }
+  __syncthreads();
+  const unsigned vm = __builtin_amdgcn_readfirstlane(rvm[slot]);
+  int xr[5], yr[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    xr[q] = rxr[slot][q];
+    yr[q] = ryr[slot][q];
+  }
+  // the union of the inside taps' columns (any row), and the rows holding one
+  int xlo = 1 << 30, xhi = -(1 << 30);
+#pragma unroll
+  for (int q = 0; q < 5; q++)
+    if ((vm >> (5 * q)) & 0x1fu) {
+      xlo = min(xlo, xr[q]);
+      xhi = max(xhi, xr[q]);
+    }
+  const int rx = z % a.aw;  // (every neighbour in the reference's camera row)
+  // the taps' columns (-2^30 outside), uniform, and the LDS byte addresses of
+  // this wave's ring and this superpixel's reference colours
+  int rcol[25];
+#pragma unroll
+  for (int t = 0; t < 25; t++) rcol[t] = __float_as_int(refc[slot][t].w);  // (VGPRs: the LDS caps the waves, not these)
+  const unsigned ring_base = (unsigned)(uintptr_t)(lds_vptr_t)&ring[w][0][0];
+  const unsigned refc_base = (unsigned)(uintptr_t)(lds_vptr_t)&refc[slot][0];
+  const int nn = sn[z];
+  float best = 1000000.0f;
+  int bi = 0x7fffffff;
+  for (int p0 = 64 * h; p0 < a.D; p0 += 64 * WPS) {
+    const int dl = p0 + lane;
+    const bool act = dl < a.D;
+    const float d = levels[act ? dl : a.D - 1];
+    // the pass's level range: (int)(d dx) is monotone in d, so a neighbour's
+    // shift range comes from its ends
+    const float dlo = wave_min_f(d), dhi = -wave_min_f(-d);
+    // the staging window of neighbour n: columns [ulo, ulo + U) of its view
+    auto window = [&](int n, int& ulo, int& U, int& sh) {
+      const int view = vs[a.V * z + n];
+      const float fdx = (float)(view % a.aw - rx);
+      sh = (int)(d * fdx);  // exact (the launcher checked the levels)
+      const int s0 = (int)(dlo * fdx), s1 = (int)(dhi * fdx);
+      const int shmin = min(s0, s1), shmax = max(s0, s1);
+      ulo = max(xlo - shmax, 0);
+      U = min(xhi - shmin, a.W - 1) - ulo + 1;
+    };
+    // stage row k = 5 n + j into slot k & 1; returns its LDS-DMA pieces (0:
+    // nothing staged -- no inside tap on the row, an empty or too wide window)
+    auto stage = [&](int n, int j, int k, int ulo, int U) -> int {
+      if (U <= 0 || !((vm >> j) & 0x108421u)) return 0;
+      U = min(U, kSwU);  // (the launcher's bound makes this a no-op; never past the slot)
+      const int view = vs[a.V * z + n];
+      const float4* row = lab + (long)view * P + (long)yr[j] * a.W + ulo;
+      const int np = (U + 63) >> 6;
+      for (int q = 0; q < np; q++) {
+        const int c0 = U >= 64 ? min(q * 64, U - 64) : 0;  // the last piece ends at U (U < 64: lanes past U re-read column U - 1)
+        glds16(row + min(c0 + lane, U - 1), &ring[w][k & 1][c0]);
+      }
+      return np;
+    };
+    float mn = 1000000.0f;
+    if (nn > 0) {
+      int ulo0, U0, sh0;
+      window(0, ulo0, U0, sh0);
+      int pcn = stage(0, 0, 0, ulo0, U0);  // pieces of the row after the one computed next
+      pcn = stage(0, 1, 1, ulo0, U0);
+      int ulo_c = ulo0, sh_c = sh0;  // the neighbour being computed
+      int ulo_s = ulo0, U_s = U0;              // the neighbour being staged (rows k + 2)
+      for (int n = 0; n < nn; n++) {
+        float ad[25];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+          const int k = 5 * n + j;
+          wait_vm(k + 1 < 5 * nn ? pcn : 0);  // row k landed (row k + 1 may still be in flight)
+          // the row's 5 taps: their columns (refc .w), then the 5 ring reads
+          // and the 5 reference colours in one asm block closed by
+          // lgkmcnt(0) -- the compiler would put vmcnt(0) (every LDS-DMA in
+          // flight, row k + 1's included) before plain LDS reads here
+          int xp[5];
+          unsigned ra[5];
+#pragma unroll
+          for (int i = 0; i < 5; i++) {
+            xp[i] = rcol[i * 5 + j] - sh_c;
+            const bool in = (unsigned)xp[i] < (unsigned)a.W;
+            ra[i] = ring_base + (unsigned)(k & 1) * (kSwU * 16u) + (in ? (unsigned)(xp[i] - ulo_c) * 16u : 0u);
+          }
+          const unsigned rb = refc_base + (unsigned)j * 16u;
+          u32x3 Bv[5];
+          f32x4 Av[5];
+          asm volatile(
+              "ds_read_b96 %0, %10\n\t"
+              "ds_read_b96 %1, %11\n\t"
+              "ds_read_b96 %2, %12\n\t"
+              "ds_read_b96 %3, %13\n\t"
+              "ds_read_b96 %4, %14\n\t"
+              "ds_read_b128 %5, %15\n\t"
+              "ds_read_b128 %6, %15 offset:80\n\t"
+              "ds_read_b128 %7, %15 offset:160\n\t"
+              "ds_read_b128 %8, %15 offset:240\n\t"
+              "ds_read_b128 %9, %15 offset:320\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(Bv[0]), "=&v"(Bv[1]), "=&v"(Bv[2]), "=&v"(Bv[3]), "=&v"(Bv[4]), "=&v"(Av[0]), "=&v"(Av[1]),
+                "=&v"(Av[2]), "=&v"(Av[3]), "=&v"(Av[4])
+              : "v"(ra[0]), "v"(ra[1]), "v"(ra[2]), "v"(ra[3]), "v"(ra[4]), "v"(rb)
+              : "memory");
+#pragma unroll
+          for (int i = 0; i < 5; i++) {
+            const bool in = (unsigned)xp[i] < (unsigned)a.W;
+            const float v = tap_ad(make_float4(Av[i].x, Av[i].y, Av[i].z, 0.f), Bv[i]);
+            ad[5 * i + j] = in ? v : -1.0f;
+          }
+          // stage row k + 2 (the next neighbour's rows 0 and 1 from j = 3 on)
+          const int k2 = k + 2;
+          int pc2 = 0;
+          if (k2 < 5 * nn) {
+            const int n2 = k2 / 5, j2 = k2 - 5 * n2;
+            if (j2 == 0) {
+              int sh2;
+              window(n2, ulo_s, U_s, sh2);
+            }
+            pc2 = stage(n2, j2, k2, ulo_s, U_s);
+          }
+          pcn = pc2;
+        }
+        float val = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 25; t++) val = tap_acc(val, ad[t], ad[t] >= 0.0f);
+        mn = val < mn ? val : mn;
+        if (n + 1 < nn) {  // the next neighbour's window (staged from j = 3 of this one)
+          ulo_c = ulo_s;
+          const int view = vs[a.V * z + n + 1];
+          sh_c = (int)(d * (float)(view % a.aw - rx));
+        }
+      }
+    }
+    if (act && mn < best) {
+      best = mn;
+      bi = dl;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob < best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    wbest[w] = best;
+    wbi[w] = bi;
+  }
+  __syncthreads();
+  if (active && h == 0 && lane == 0) {
+    for (int k = 1; k < WPS; k++) {
       const float ob = wbest[w + k];
       const int oi = wbi[w + k];
       if (ob < best || (ob == best && oi < bi)) {
@@ -814,8 +1073,7 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
   if (z1 <= z0) return 0;
   // k_sweep_spixl's 32-bit byte offsets within a view (a re-laid one spans
   // at most (W + H) H elements)
-  if ((long)(W + H) * H * 16 >= (1L << 31) || W >= (1 << 23) || H >= (1 << 23))  // (+ its 24-bit multiplies)
-    return arg_fail("superpixel sweep: image too large for 32-bit offsets");
+  if ((long)(W + H) * H * 16 >= (1L << 31)) return arg_fail("superpixel sweep: image too large for 32-bit offsets");
   hipStream_t s = ctx->stream;
   int mw = map_dim(W, S), mh = map_dim(H, S);
   long M = (long)mw * mh;
@@ -892,6 +1150,35 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
         if (!(fabsf(f) < 16777216.0f) || f != truncf(f)) hz = false;
       }
     }
+  // HZ with 64 levels per wave: the LDS-staged rows (MVS_SWEEP_RING=0, read per call: the gathers)
+  const char* re = getenv("MVS_SWEEP_RING");
+  bool ring_ok = hz && !half && !(re && atoi(re) == 0);
+  if (ring_ok) {  // every staged window fits kSwU columns (see k_sweep_spixl_ring)
+    float rng = 0.0f;
+    for (int c0 = 0; c0 < D; c0 += 64) {
+      float lo = ctx->h_levels[c0], hi = lo;
+      for (int l = c0; l < std::min(D, c0 + 64); l++) {
+        lo = std::min(lo, ctx->h_levels[l]);
+        hi = std::max(hi, ctx->h_levels[l]);
+      }
+      rng = std::max(rng, hi - lo);
+    }
+    int mdx = 0;
+    for (int z = z0; z < z1; z++)
+      for (int k = 0; k < ctx->h_sn[z]; k++) mdx = std::max(mdx, std::abs(ctx->h_vs[(size_t)V * z + k] % aw - z % aw));
+    if (2.0 * (S - 1) + 2.0 + (double)rng * mdx + 1.0 > (double)kSwU) ring_ok = false;
+  }
+  if (ring_ok) {
+    const dim3 g((unsigned)(8 * ((nb + 7) / 8)), (unsigned)(z1 - z0));
+    if (wps == 1)
+      hipLaunchKernelGGL(k_sweep_spixl_ring<1>, g, dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a);
+    else if (wps == 2)
+      hipLaunchKernelGGL(k_sweep_spixl_ring<2>, g, dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a);
+    else
+      hipLaunchKernelGGL(k_sweep_spixl_ring<4>, g, dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a);
+    MVS_LAUNCH_CHECK("k_sweep_spixl_ring");
+    return 0;
+  }
   auto kern = labT ? (half ? k_sweep_spixl<32, true> : k_sweep_spixl<64, true>)
               : hz ? (half ? k_sweep_spixl<32, false, true> : k_sweep_spixl<64, false, true>)
                    : (half ? k_sweep_spixl<32, false> : k_sweep_spixl<64, false>);

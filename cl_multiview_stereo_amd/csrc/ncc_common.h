@@ -69,6 +69,12 @@ __device__ __forceinline__ float vmin3(float a, float b, float c) {
   asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+// IEEE 754-2019 maximum of three (gfx950): NaN when any operand is NaN
+__device__ __forceinline__ float vmaximum3(float a, float b, float c) {
+  float r;
+  asm("v_maximum3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 // median of three: with lo <= hi, med3(lo, hi, c) = min(hi, max(lo, c))
 __device__ __forceinline__ float vmed3(float lo, float hi, float c) {
   float r;

@@ -238,7 +238,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
           for (int db = 0; db < NDB; db++) {
             const f32x2 e = f32x2{E[xb][yb][db][r], E[xb][yb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
-            cst[db] = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
+            // NDB = 2: 1 - m without the clamp max(-1, m) -- a cost above 2 or
+            // NaN (no valid neighbour window at the level) stands for the
+            // clamped 2, restored at the merge; the pair fold below treats NaN
+            // as absent.  (NDB = 1 keeps the clamp: its med3 fold would not.)
+            if constexpr (NDB == 2)
+              cst[db] = f32x2{1.0f, 1.0f} - e;
+            else
+              cst[db] = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
             if (TAIL) cst[db] += f32x2{kill[db], kill[db]};  // costs are >= 0: x + 0 = x, x + inf = inf
           }
 #pragma unroll
@@ -248,10 +255,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             float& v0 = wv0[xb][yb][r + h];
             float& v1 = wv1[xb][yb][r + h];
             if constexpr (NDB == 2) {
-              const float c0 = cst[0][h], c1 = cst[NDB - 1][h];  // never NaN: 1 - max(-1, NaN) = 2
-              const float lo = vmin(c0, c1), hi = vmax(c0, c1);
-              const unsigned idx = c1 < c0 ? d1 : d0;
-              v1 = vmin3(vmax(v0, lo), v1, hi);
+              const float c0 = cst[0][h], c1 = cst[NDB - 1][h];  // NaN: absent (the clamped 2)
+              const float lo = vmin3(c0, c1, INFINITY);  // the smaller present cost (+inf: none)
+              const float hi = vmaximum3(c0, c1, c1);    // the larger, NaN if either is absent
+              const unsigned idx = lo == c0 ? d0 : d1;   // a tie keeps the lower level
+              v1 = vmin3(vmax(v0, lo), v1, hi);          // (a NaN hi drops out of the min)
               wp = lo < v0 ? (wp & ~hm) | (idx & hm) : wp;
               v0 = vmin(v0, lo);
             } else {  // one level: the sequential fold
@@ -423,10 +431,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         const float v = (unsigned)(i - (int)bi + 1) <= 2u ? m1[w * kMfMergeStride + q] : m0[w * kMfMergeStride + q];
         c2 = vmin(c2, v);
       }
+      // The fold skipped the clamp (cost = 1 - max(-1, m) = min(2, 1 - m)).
+      // If the smallest cost is below 2 the clamp changes neither it nor its
+      // level, and the second smallest outside bi +- 1 is min(2, that) whenever
+      // such a level exists; otherwise every level costs 2 and the first level
+      // wins with confidence 0 (k_wta's strict <, in level order).
+      const bool all2 = !(bv < 2.0f);
+      const int b = (int)bi;
+      if (!all2 && a.D > min(b + 1, a.D - 1) - max(b - 1, 0) + 1) c2 = vmin(c2, 2.0f);
       if (xx < W && yy < H) {
         const long p = P * ref + (long)yy * W + xx;
-        wo.disp[p] = (int)bi >= 0 ? wo.levels[bi] : 0.0f;
-        if (wo.conf) wo.conf[p] = ((int)bi < 0 || c2 == kWtaInit) ? 0.0f : c2 - bv;
+        wo.disp[p] = a.D <= 0 ? 0.0f : wo.levels[all2 ? 0 : b];
+        if (wo.conf) wo.conf[p] = (all2 || c2 == kWtaInit) ? 0.0f : c2 - bv;
       }
     }
     __syncthreads();

@@ -38,6 +38,7 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* out, unsigned a, u
     p[i] = f2{(float)v[i], (float)(v[i] + 1)};
   }
   const float fa = __int_as_float(a);
+  unsigned long long msk = __builtin_amdgcn_read_exec() & (unsigned long long)(a * 0x9e3779b97f4a7c15ull), m2 = 0;
   const f2 pa = f2{fa, fa};
   if (threadIdx.x == 1u << 30) lds_pad[0] = 1;  // keep the LDS allocation
   __builtin_amdgcn_s_waitcnt(0);
@@ -59,7 +60,17 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* out, unsigned a, u
     if (OP == 10) asm volatile("v_add_f32_e64 %0, %1, %0" : "+v"(v[i]) : "v"(fa));                                \
     if (OP == 11) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(v[i]) : "v"(fa), "v"(fa));                          \
     if (OP == 12) asm volatile("v_med3_f32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(fa), "v"(fa));                      \
-    if (OP == 13) asm volatile("v_max_i32 %0, %1, %0" : "+v"(v[i]) : "v"(a));
+    if (OP == 13) asm volatile("v_max_i32 %0, %1, %0" : "+v"(v[i]) : "v"(a));                                    \
+    if (OP == 14) asm volatile("v_max3_f32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(fa), "v"(fa));                     \
+    if (OP == 15) asm volatile("v_min_f32 %0, %1, %0" : "+v"(v[i]) : "v"(fa));                                   \
+    if (OP == 16) asm volatile("v_max_f32_e64 %0, %1, %0" : "+v"(v[i]) : "v"(fa));                               \
+    if (OP == 17) asm volatile("v_sub_f32 %0, %1, %0" : "+v"(v[i]) : "v"(fa));                                   \
+    if (OP == 18) asm volatile("v_cndmask_b32 %0, %1, %0, vcc" : "+v"(v[i]) : "v"(a));                           \
+    if (OP == 19) asm volatile("v_min3_f32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(fa), "v"(fa));                     \
+    if (OP == 20) asm volatile("v_cndmask_b32_e64 %0, %1, %0, %2" : "+v"(v[i]) : "v"(a), "s"(msk));              \
+    if (OP == 21) asm volatile("v_cmp_lt_f32 vcc, %1, %0\n\tv_cndmask_b32 %0, %1, %0, vcc" : "+v"(v[i]) : "v"(fa) : "vcc"); \
+    if (OP == 22) asm volatile("v_bfi_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(a), "v"(fa));                       \
+    if (OP == 23) asm volatile("v_cmp_lt_f32_e64 %1, %2, %0\n\tv_cndmask_b32_e64 %0, %2, %0, %1" : "+v"(v[i]), "=s"(m2) : "v"(fa));
 #pragma unroll
     for (int u = 0; u < 4; u++) { REP8(STEP) }
 #undef STEP
@@ -71,6 +82,7 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* out, unsigned a, u
   const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
   unsigned s = 0;
   for (int i = 0; i < 8; i++) s += v[i] + __float_as_uint(p[i].x) + __float_as_uint(p[i].y);
+  s += (unsigned)m2 + (unsigned)msk;
   const unsigned wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if ((threadIdx.x & 63) == 0) {
     out[5 * wave + 0] = t0;
@@ -170,6 +182,16 @@ int main() {
     rep("v_fmac_f32", w, run<11>(out, cus, w, 0x3f800001u, 7u, iters));
     rep("v_med3_f32", w, run<12>(out, cus, w, 0x3f800001u, 7u, iters));
     rep("v_max_i32", w, run<13>(out, cus, w, 3u, 7u, iters));
+    rep("v_max3_f32", w, run<14>(out, cus, w, 0x3f800001u, 7u, iters));
+    rep("v_min_f32", w, run<15>(out, cus, w, 0x3f800001u, 7u, iters));
+    rep("v_max_f32_e64", w, run<16>(out, cus, w, 0x3f800001u, 7u, iters));
+    rep("v_sub_f32", w, run<17>(out, cus, w, 0x3f800001u, 7u, iters));
+    rep("v_cndmask_b32", w, run<18>(out, cus, w, 3u, 7u, iters));
+    rep("v_min3_f32", w, run<19>(out, cus, w, 0x3f800001u, 7u, iters));
+    rep("cndmask_e64_s", w, run<20>(out, cus, w, 3u, 7u, iters));
+    rep("cmp+cndmask_vcc", w, run<21>(out, cus, w, 0x3f800001u, 7u, iters));
+    rep("v_bfi_b32", w, run<22>(out, cus, w, 3u, 7u, iters));
+    rep("cmp+cndmask_s", w, run<23>(out, cus, w, 0x3f800001u, 7u, iters));
   }
   return 0;
 }

@@ -420,8 +420,20 @@ def bench(args, world, rank, local):
 
     pipe, step = make(fused, conc_head)
     recording[0] = True
+    # the fused sweep's own dispatch time as well (events of its launches,
+    # hipExtLaunchKernel): an event recorded on the stream before a call can
+    # fire while the previous kernel still runs (the ring sweep, ~0.16 ms), so
+    # the call-bracketing events read ~5 % high (profiles/r05/headline_check.json)
+    ktimes, kviews = None, 0
+    views0 = calls["fused_views"]
+    if fused and hasattr(e, "set_kernel_timing"):
+        e.set_kernel_timing(True)
     elapsed, out = timed(step, args.steps, args.warmup, dev, world, sync)
     recording[0] = False
+    if fused and hasattr(e, "set_kernel_timing"):
+        ktimes = e.kernel_times()
+        kviews = calls["fused_views"] - views0  # the views those launches swept (warmup + timed steps)
+        e.set_kernel_timing(False)
     ms_per_step = elapsed * 1e3 / max(args.steps, 1)
     units = V if sharded else world * V  # reference views processed per step, whole job
     mpix = units * W * H * args.steps / elapsed / 1e6
@@ -504,6 +516,10 @@ def bench(args, world, rank, local):
             "view_cells_per_s": round(cells * nbr * vpc / t_f / 1e9, 3), "unit_view_cells": "G view-cells/s",
             "timing": "HIP events around each mvs_ncc_wta_range_d call of the timed steps, on its stream" +
                       (" (the serial_variant pass: one stream, the kernel alone on the GPU)" if conc_head else "")}
+        if ktimes and kviews > 0 and not conc_head:
+            res["roofline_sweep"]["kernel_avg_ms_per_view"] = round(sum(ktimes) / kviews, 4)
+            res["roofline_sweep"]["kernel_timing"] = ("start / stop events of each fused launch's own dispatch "
+                                                      "(hipExtLaunchKernel), warmup + timed steps")
         if per_view is not None and not per_view.get("stale"):
             res["roofline_sweep"].update({
                 "valu_wave_insts_per_view": round(per_view["insts"]),
@@ -519,6 +535,13 @@ def bench(args, world, rank, local):
                 vp = sum(n for _, _, n in tm["fused"]) / len(tm["fused"])
                 return tf, vp
             t_h, v_h = form(form_timers) if form_timers["fused"] else (t_f, vpc)
+            t_ev = t_h
+            # the kernel's own dispatch time per call when recorded (warmup + timed
+            # calls alike: every recorded call's views over every recorded launch)
+            kview = None
+            if ktimes and form_timers["fused"] and not conc_head and kviews > 0:
+                kview = sum(ktimes) * 1e-3 / kviews
+                t_h = kview * v_h
             issue = per_view["insts"] + 2.0 * per_view.get("mfma", 0.0)  # an MFMA holds VALU issue for 8 cycles
             ach = issue * v_h / t_h / 1e9
             rh = {"bound": "valu", "kernel": per_view["kernel"],
@@ -528,9 +551,12 @@ def bench(args, world, rank, local):
                   "algorithmic": f"{round(per_view['insts'])} VALU wave-instructions per reference view"
                                  + (f" + 2 x {round(per_view['mfma'])} MFMA (8 issue cycles each)"
                                     if per_view.get("mfma") else "")
-                                 + f" (SQ_INSTS_VALU of its own PMC pass, {per_view['source']}) over the HIP-event "
-                                   f"time per view of the headline pass",
-                  "avg_ms_per_view": round(t_h * 1e3 / v_h, 4), "peak_basis": VALU_PEAK_NOTE}
+                                 + f" (SQ_INSTS_VALU of its own PMC pass, {per_view['source']}) over the "
+                                 + ("kernel's own dispatch time per view (start / stop events of its launches, "
+                                    "hipExtLaunchKernel)" if kview is not None else "HIP-event time per view")
+                                 + " in the headline pass",
+                  "avg_ms_per_view": round(t_h * 1e3 / v_h, 4),
+                  "event_avg_ms_per_view": round(t_ev * 1e3 / v_h, 4), "peak_basis": VALU_PEAK_NOTE}
             if conc_head:
                 rh["serial_form"] = {"avg_ms_per_view": round(t_f * 1e3 / vpc, 4),
                                      "frac": round(issue * vpc / t_f / VALU_PEAK, 4)}

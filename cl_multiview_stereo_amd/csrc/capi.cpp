@@ -176,6 +176,10 @@ void mvs_destroy(mvs_ctx* c) {
   if (c->d_vs) hipFree(c->d_vs);
   if (c->d_sn) hipFree(c->d_sn);
   for (auto& kv : c->plans) hipFree(kv.second);
+  for (auto& ev : c->kev) {
+    hipEventDestroy(ev.first);
+    hipEventDestroy(ev.second);
+  }
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -322,6 +326,27 @@ int mvs_set_ncc_variant(mvs_ctx* c, int waves, int levels_per_wave, int band_w, 
   c->ncc_dpw = levels_per_wave;
   c->ncc_bw = band_w;
   c->ncc_general = general_rows ? 1 : 0;
+  return 0;
+}
+
+int mvs_set_kernel_timing(mvs_ctx* c, int on) {
+  if (!c) return mvs::arg_fail("mvs_set_kernel_timing: null context");
+  c->ktime = on != 0;
+  c->kev_used = 0;
+  return 0;
+}
+
+int mvs_kernel_times(mvs_ctx* c, float* ms, int cap, int* n) {
+  if (!c || !n || (cap > 0 && !ms)) return mvs::arg_fail("mvs_kernel_times: bad arguments");
+  const int k = (int)c->kev_used;
+  for (int i = 0; i < k && i < cap; i++) {
+    MVS_HIP(hipEventSynchronize(c->kev[i].second), "hipEventSynchronize(kernel timing)");
+    float t = 0.0f;
+    MVS_HIP(hipEventElapsedTime(&t, c->kev[i].first, c->kev[i].second), "hipEventElapsedTime(kernel timing)");
+    ms[i] = t;
+  }
+  *n = k;
+  c->kev_used = 0;
   return 0;
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -33,9 +34,25 @@ struct mvs_ctx {
   // variant of the last launch {K, TH, DPW, NW, BW, PAR, FUSE, NB} (DPW 16: the matrix-core form)
   int ncc_nw = 0, ncc_dpw = 0, ncc_bw = 0, ncc_general = 0;
   int ncc_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // kernel timing (mvs_set_kernel_timing): the fused NCC sweep's launches carry
+  // start / stop events of their own dispatch (hipExtLaunchKernel), pooled
+  bool ktime = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;
+  size_t kev_used = 0;
 };
 
 namespace mvs {
+
+// the next timed launch's event pair (null, null: timing off or no events)
+inline std::pair<hipEvent_t, hipEvent_t> kernel_events(mvs_ctx* ctx) {
+  if (!ctx->ktime) return {nullptr, nullptr};
+  if (ctx->kev_used == ctx->kev.size()) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return {nullptr, nullptr};
+    ctx->kev.push_back({a, b});
+  }
+  return ctx->kev[ctx->kev_used++];
+}
 
 void set_error(const std::string& msg);
 int hip_fail(hipError_t e, const char* what);

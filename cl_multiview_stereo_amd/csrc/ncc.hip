@@ -613,7 +613,8 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
             "hipFuncSetAttribute(ncc lds)");
     lds_set[vol ? 0 : 1] = lds;
   }
-  hipLaunchKernelGGL(kern, g, dim3(NW * 64), lds, s, stats, pk, plan, a, vol, wo);
+  const auto ev = vol ? std::pair<hipEvent_t, hipEvent_t>{nullptr, nullptr} : kernel_events(ctx);  // (the fused sweep only)
+  hipExtLaunchKernelGGL(kern, g, dim3(NW * 64), lds, s, ev.first, ev.second, 0, stats, pk, plan, a, vol, wo);
   MVS_LAUNCH_CHECK(vol ? "k_ncc_volume" : "k_ncc_volume (fused WTA)");
   return 0;
 }

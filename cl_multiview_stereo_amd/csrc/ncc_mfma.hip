@@ -469,7 +469,9 @@ int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccM
             "hipFuncSetAttribute(ncc mfma lds)");
     lds_set = lds;
   }
-  hipLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(512), lds, ctx->stream, stats, pk, plan, a, wo);
+  const auto ev = kernel_events(ctx);  // (timing off: plain launch)
+  hipExtLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(512), lds, ctx->stream, ev.first, ev.second, 0, stats, pk,
+                        plan, a, wo);
   MVS_LAUNCH_CHECK("k_ncc_mfma (fused WTA)");
   return 0;
 }

@@ -224,6 +224,17 @@ class Engine:
         _lib.check(self.L.mvs_set_ncc_variant(self.ctx, int(waves), int(levels_per_wave), int(band_w),
                                               int(bool(general_rows))), "mvs_set_ncc_variant")
 
+    def set_kernel_timing(self, on: bool) -> None:
+        """Record start / stop events of every fused NCC sweep launch's own dispatch (bench aid)."""
+        _lib.check(self.L.mvs_set_kernel_timing(self.ctx, int(bool(on))), "mvs_set_kernel_timing")
+
+    def kernel_times(self, cap: int = 8192) -> list:
+        """The recorded fused-sweep launches' kernel times in ms (waits for them; starts a new record)."""
+        buf = (C.c_float * cap)()
+        n = C.c_int(0)
+        _lib.check(self.L.mvs_kernel_times(self.ctx, buf, cap, C.byref(n)), "mvs_kernel_times")
+        return list(buf[:min(n.value, cap)])
+
     def ncc_last_variant(self) -> dict:
         """The last NCC launch: K, tile rows, levels per wave, waves, band width,
         PAR (row parity: 0 mixed, 1 every band row pair-aligned, 2 odd pk / even

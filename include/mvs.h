@@ -187,6 +187,15 @@ int mvs_ncc_wta_range_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int
  * (1 single-buffered, 2 double-buffered)}: eight int32. */
 int mvs_set_ncc_variant(mvs_ctx* ctx, int waves, int levels_per_wave, int band_w, int general_rows);
 int mvs_ncc_last_variant(mvs_ctx* ctx, int32_t* out8);
+/* Kernel timing (a measurement aid, no reference counterpart): with timing on,
+ * every fused NCC sweep launch (mvs_ncc_wta_d / mvs_ncc_wta_range_d) records
+ * start / stop events of its own dispatch (hipExtLaunchKernel), so the time is
+ * the kernel's alone -- an event recorded on the stream before a call can fire
+ * while the previous kernel is still running.  mvs_kernel_times waits for the
+ * recorded launches and returns their times in ms (up to cap of them; *n = how
+ * many were recorded), then starts a new record; switching timing on also does. */
+int mvs_set_kernel_timing(mvs_ctx* ctx, int on);
+int mvs_kernel_times(mvs_ctx* ctx, float* ms, int cap, int* n);
 
 /* Superpixel-plane refinement (clDepthRefinement, depth_refinement.cpp:91-1470).
  * flat [V][mh][mw][2] and state/state2 [V][mh][mw][6] are caller-provided

@@ -606,6 +606,7 @@ typedef struct {
  *                           (the form the SLIC centre means are pinned to)
  *   MVS_PROBE_LIBM_EXP      exp / expf from the C library (glibc) instead of mvs_detmath
  *   MVS_PROBE_EXP_ULP=k     every expf result moved by a hash-chosen -k..+k ulp
+ *   MVS_PROBE_EXP_SEED=s    (with EXP_ULP) another draw of that hash (0: the default)
  *   MVS_PROBE_SQRT_RSQ      sqrt(s) as s * RN(1/sqrt(s)) (an rsqrt-based sqrt)
  *   MVS_PROBE_REFINE_CONTRACT  (clang -mfma) mul+add contracted from here on */
 #ifdef MVS_PROBE_REFINE_CONTRACT
@@ -634,7 +635,10 @@ static float rexpf(float x) {
 #ifdef MVS_PROBE_EXP_ULP
   uint32_t u, v;
   memcpy(&u, &x, 4);
-  u = (u ^ (u >> 15)) * 2654435761u;
+#ifndef MVS_PROBE_EXP_SEED
+#define MVS_PROBE_EXP_SEED 0
+#endif
+  u = (u ^ (u >> 15) ^ ((uint32_t)MVS_PROBE_EXP_SEED * 0x9E3779B9u)) * 2654435761u;  /* seed 0: the round-4 draw */
   int k = (int)((u >> 8) % (2 * MVS_PROBE_EXP_ULP + 1)) - MVS_PROBE_EXP_ULP;
   if (r > 0.0f && r < 3.0e38f) {
     memcpy(&v, &r, 4);

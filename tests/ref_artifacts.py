@@ -287,6 +287,10 @@ PROBE_BUILDS = {  # oracle/Makefile `probes`, MVS_PROBE_* in oracle/mvs_oracle.c
     "rcontract": "mul+add contracted (FMA) in the refinement only",
     "rsys": "the systematic alternatives together: rcpdiv + libmexp + sqrtrsq + rcontract",
     "rall": "all of the above together (ulp 1)",
+    # other draws of the ulp hash (one draw is a sample, not a bound)
+    "expulp1s1": "expf -1..+1 ulp, hash seed 1", "expulp1s2": "expf -1..+1 ulp, hash seed 2",
+    "expulp1s3": "expf -1..+1 ulp, hash seed 3", "expulp2s1": "expf -2..+2 ulp, hash seed 1",
+    "expulp2s2": "expf -2..+2 ulp, hash seed 2", "expulp2s3": "expf -2..+2 ulp, hash seed 3",
 }
 
 
@@ -457,7 +461,7 @@ def main():
         return
     if a.probes:
         res = score_probes()
-        out = a.out or os.path.join(ROOT, "profiles", "r04", "ref_probes.json")
+        out = a.out or os.path.join(ROOT, "profiles", "r05", "ref_probes.json")
         with open(out, "w") as f:
             json.dump(res, f, indent=1)
         print("wrote", out)

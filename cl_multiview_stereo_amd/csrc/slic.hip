@@ -989,10 +989,12 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
     pres &= pres - 1;
     const int i1 = pres ? __builtin_ctz(pres) : i0;  // i1 == i0: a second copy, not stored
     pres &= pres ? pres - 1 : 0u;
-    float sL[2], sa[2], sb[2];
-    uint32_t sq[2];
+    float sL[2] = {0.f, 0.f}, sa[2] = {0.f, 0.f}, sb[2] = {0.f, 0.f};
+    uint32_t sq[2] = {0u, 0u};
+    const bool two = i1 != i0;  // (uniform) a single cell: its second copy is neither summed nor stored
 #pragma unroll
     for (int h = 0; h < 2; h++) {  // the in-lane step of the trees
+      if (h == 1 && !two) break;
       const int i = h == 0 ? i0 : i1;
       bool mem[4];
 #pragma unroll
@@ -1012,9 +1014,8 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
       sb[h] = (vb[0] + vb[2]) + (vb[1] + vb[3]);
     }
     const float T1 = wave_tree4s(sL[0], sa[0], sb[0], sL[1]);  // lanes 0: L0, 32: a0, 16: b0, 48: L1
-    const float T2 = wave_tree2s(sa[1], sb[1]);                // lanes 0: a1, 32: b1
+    const float T2 = two ? wave_tree2s(sa[1], sb[1]) : 0.f;    // lanes 0: a1, 32: b1
     const uint32_t Q = wave_sum2_u32(sq[0], sq[1]);            // lane 32 h: cell h's x, y, count
-    const bool two = i1 != i0;
     int base[2];  // (records of one view: the launcher checks the size)
 #pragma unroll
     for (int h = 0; h < 2; h++) {

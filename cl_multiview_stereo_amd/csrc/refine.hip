@@ -1176,8 +1176,11 @@ constexpr int RI_WIN = 5;
 constexpr int8_t RI_OVER = -128;  // first term not yet counted (|term| <= 32)
 // reference-independent per-pixel candidate lists (see k_remove_incons_q)
 struct RiShared {
-  float sv[RI_MAXV][64];   // distinct candidates, descending
-  float srt[RI_MAXV][64];  // the sorted list (preparation only)
+  float sv[RI_MAXV][64];  // distinct candidates, descending
+  union {
+    float srt[RI_MAXV][64];     // the sorted list (preparation only)
+    uint32_t iv[RI_MAXV][64];   // then each distinct candidate's in-image camera offsets (ri_span_ends)
+  };
   int8_t a[RI_MAXV][64];   // first stability term of each distinct candidate
   int nd[64];              // distinct candidates per pixel
 };
@@ -1236,7 +1239,11 @@ __device__ __forceinline__ void ri_prep(RiShared& S, const float* __restrict__ p
 // its ends come from one reciprocal with a 1e-3 margin (dd * k is within
 // 2^-23 of the product, and only |k| <= 8 matters), so the count can only
 // come out high.  dd != 0 (candidates are nonzero).
-__device__ __forceinline__ int in_span_ub(float dd, float p, int lim, int k0, int k1) {
+// The interval's ends do not depend on the reference view (k0, k1 do): they
+// are computed once per (pixel, candidate) for the workgroup's references,
+// as int8 (|k0|, |k1| < RI_MAXV, so clamping the ends to [-128, 127] changes
+// no count), packed (ceil end, floor end) in the low 16 bits.
+__device__ __forceinline__ uint32_t ri_span_ends(float dd, float p, int lim) {
   const float r = __builtin_amdgcn_rcpf(dd);
   float lo = (p - (float)lim + 0.5f) * r, hi = (p + 0.5f) * r;
   if (dd < 0.0f) {
@@ -1244,9 +1251,12 @@ __device__ __forceinline__ int in_span_ub(float dd, float p, int lim, int k0, in
     lo = hi;
     hi = t;
   }
-  lo = fminf(fmaxf(lo - 1e-3f, -1.0e6f), 1.0e6f);
-  hi = fminf(fmaxf(hi + 1e-3f, -1.0e6f), 1.0e6f);
-  const int kl = max(k0, (int)ceilf(lo)), kh = min(k1, (int)floorf(hi));
+  lo = fminf(fmaxf(lo - 1e-3f, -128.0f), 127.0f);
+  hi = fminf(fmaxf(hi + 1e-3f, -128.0f), 127.0f);
+  return ((uint32_t)(int)ceilf(lo) & 0xffu) | ((uint32_t)(int)floorf(hi) & 0xffu) << 8;
+}
+__device__ __forceinline__ int ri_span_count(uint32_t e, int k0, int k1) {
+  const int kl = max(k0, (int)(int8_t)(e & 0xffu)), kh = min(k1, (int)(int8_t)((e >> 8) & 0xffu));
   return max(0, kh - kl + 1);
 }
 
@@ -1269,9 +1279,16 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
   }
   if (wave == 0) ri_prep(S, proj, PP, p, xin, V, fuse, lane);
   __syncthreads();
+  if (inb) {  // the candidates' in-image intervals (over srt: the preparation is done), dealt over the waves
+    const int ndl = S.nd[lane];
+    for (int q = wave; q < ndl; q += RG) {
+      const float dv = S.sv[q][lane];
+      S.iv[q][lane] = ri_span_ends(dv, (float)x, W) | ri_span_ends(bl * dv, (float)y, H) << 16;
+    }
+    __syncthreads();
+  }
   const int r = z0 + RG * fg.g + wave;
-  if (r >= z1 || !xin) return;  // after the only barrier
-  const float xf = (float)x, yf = (float)y;
+  if (r >= z1 || !xin) return;  // after the barriers
   const unsigned P4 = (unsigned)(P * 4);  // the launcher checks V * P * 4 < 2^31
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)full, 0, 0x7fffffff, 0x00020000);
   const int nd = S.nd[lane];
@@ -1287,8 +1304,10 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
   // decided either way.  The camera grid is aw x (V / aw) (inb = 0 otherwise).
   const int cr = z0 + RG * fg.g + wave;
   const int crx = cr % aw, cry = cr / aw, ah = V / aw;
-  auto bound = [&](float dv, float bdv) {
-    return inb ? in_span_ub(dv, xf, W, -crx, aw - 1 - crx) * in_span_ub(bdv, yf, H, -cry, ah - 1 - cry) : V;
+  auto bound = [&](int c) {
+    if (!inb) return V;
+    const uint32_t e = S.iv[c][lane];
+    return ri_span_count(e, -crx, aw - 1 - crx) * ri_span_count(e >> 16, -cry, ah - 1 - cry);
   };
   auto take = [&](int s) {  // hand candidate nxt to slot s (k = nd: idle)
     k[s] = nd;
@@ -1297,7 +1316,7 @@ __global__ __launch_bounds__(64 * RG) void k_remove_incons_q(const float* __rest
       const float dv = S.sv[c][lane];
       const int a = S.a[c][lane];
       const float bdv = bl * dv;
-      const int nb = bound(dv, bdv);
+      const int nb = bound(c);
       if (a + nb < 0) continue;  // unstable whatever the gathers say
       k[s] = c;
       d[s] = dv;

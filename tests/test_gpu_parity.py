@@ -400,6 +400,25 @@ def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns, bound):
     assert_bits(out.cpu().numpy(), oout, f"filter output ({kern}, FB {fb})")
 
 
+@pytest.mark.parametrize("fb,ns", [(2, 2), (4, 1)])
+def test_filter_ragged_grid(engine, monkeypatch, fb, ns):
+    # V = 27 views on rows of aw = 6 (the last camera row holds 3): the queue
+    # walk's row-shared (FB 2) and per-view (FB 4) offsets over j < V, without
+    # the in-image bounds (they assume a complete aw x (V / aw) grid)
+    V, aw, H, W = 27, 6, 20, 72
+    rng = np.random.default_rng(27 + fb)
+    base = rng.integers(2, 12, size=(V, 1, 1)).astype(np.float32)
+    disp = base + rng.choice(np.float32([0.0, 0.25, 0.5, 1.0, 1.5, 6.0]), size=(V, H, W))
+    disp[rng.random(disp.shape) < 0.1] = 0.0
+    monkeypatch.setenv("MVS_FILTER_KERNEL", "q")
+    monkeypatch.setenv("MVS_FILTER_FB", str(fb))
+    monkeypatch.setenv("MVS_FILTER_NS", str(ns))
+    proj, out = engine.filter(dev(disp), aw, 1.0359, 1.0)
+    oproj, oout = orc.filt(disp, aw, 1.0359, 1.0)
+    assert_bits(proj.cpu().numpy(), oproj, "filter projection")
+    assert_bits(out.cpu().numpy(), oout, f"filter output (ragged grid, FB {fb})")
+
+
 @pytest.mark.parametrize("kern,aw,ah", [("q", 3, 2), ("q", 4, 3), ("q", 8, 4), ("q", 9, 5), ("q", 10, 7),
                                          ("px", 8, 4)])
 def test_filter_row_bands(engine, monkeypatch, aw, ah, kern):

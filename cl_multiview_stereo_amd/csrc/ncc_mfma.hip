@@ -413,22 +413,38 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
       // largest level (it only ever comes with the initial cost 1e6, which no
       // real level has).  Costs can be slightly negative (NCC rounding past 1),
       // so they are compared as floats.
-      float bv = m0[q];
-      unsigned bi = (unsigned)mi[q];
+      // every class's entries read up front (one LDS latency, not one per
+      // class), the minimum as a branch-free tree (the order is immaterial:
+      // the classes' levels are distinct, so no two entries tie in both keys)
+      float v0s[16], v1s[16];
+      unsigned is[16];
 #pragma unroll
-      for (int w = 1; w < 16; w++) {
-        const float v = m0[w * kMfMergeStride + q];
-        const unsigned i = (unsigned)mi[w * kMfMergeStride + q];
-        if (v < bv || (v == bv && i < bi)) {
-          bv = v;
-          bi = i;
-        }
+      for (int w = 0; w < 16; w++) {
+        v0s[w] = m0[w * kMfMergeStride + q];
+        is[w] = (unsigned)mi[w * kMfMergeStride + q];
+        v1s[w] = m1[w * kMfMergeStride + q];
       }
+      float tv[16];
+      unsigned ti[16];
+#pragma unroll
+      for (int w = 0; w < 16; w++) {
+        tv[w] = v0s[w];
+        ti[w] = is[w];
+      }
+#pragma unroll
+      for (int h = 8; h >= 1; h >>= 1)
+#pragma unroll
+        for (int w = 0; w < h; w++) {
+          const bool tk = (tv[w + h] < tv[w]) | ((tv[w + h] == tv[w]) & (ti[w + h] < ti[w]));
+          tv[w] = tk ? tv[w + h] : tv[w];
+          ti[w] = tk ? ti[w + h] : ti[w];
+        }
+      const float bv = tv[0];
+      const unsigned bi = ti[0];
       float c2 = kWtaInit;
 #pragma unroll
       for (int w = 0; w < 16; w++) {
-        const int i = mi[w * kMfMergeStride + q];
-        const float v = (unsigned)(i - (int)bi + 1) <= 2u ? m1[w * kMfMergeStride + q] : m0[w * kMfMergeStride + q];
+        const float v = (unsigned)((int)is[w] - (int)bi + 1) <= 2u ? v1s[w] : v0s[w];
         c2 = vmin(c2, v);
       }
       // The fold skipped the clamp (cost = 1 - max(-1, m) = min(2, 1 - m)).

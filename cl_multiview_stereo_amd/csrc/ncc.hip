@@ -502,22 +502,28 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     __syncthreads();
     for (int q = tid; q < TP; q += NW * 64) {
       const int xx = x0 + (q & 63), yy = y0 + (q >> 6);
-      float bv = m0[q];
-      int bi = mi[q];
+      // every wave's entries read up front (one LDS latency, not one per
+      // wave) and compared without branches, in wave order as before
+      float v0s[NW], v1s[NW];
+      int is[NW];
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        v0s[w] = m0[w * TP + q];
+        is[w] = mi[w * TP + q];
+        v1s[w] = m1[w * TP + q];
+      }
+      float bv = v0s[0];
+      int bi = is[0];
 #pragma unroll
       for (int w = 1; w < NW; w++) {
-        const float v = m0[w * TP + q];
-        const int i = mi[w * TP + q];
-        if (v < bv || (v == bv && i >= 0 && i < bi)) {
-          bv = v;
-          bi = i;
-        }
+        const bool tk = (v0s[w] < bv) | ((v0s[w] == bv) & (is[w] >= 0) & (is[w] < bi));
+        bv = tk ? v0s[w] : bv;
+        bi = tk ? is[w] : bi;
       }
       float c2 = kWtaInit;
 #pragma unroll
       for (int w = 0; w < NW; w++) {
-        const int i = mi[w * TP + q];
-        const float v = (i >= bi - 1 && i <= bi + 1) ? m1[w * TP + q] : m0[w * TP + q];
+        const float v = ((is[w] >= bi - 1) & (is[w] <= bi + 1)) ? v1s[w] : v0s[w];
         c2 = vmin(c2, v);
       }
       if (xx < W && yy < H) {

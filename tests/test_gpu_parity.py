@@ -400,6 +400,24 @@ def test_filter_variants(engine, monkeypatch, aw, ah, kern, fb, ns, bound):
     assert_bits(out.cpu().numpy(), oout, f"filter output ({kern}, FB {fb})")
 
 
+@pytest.mark.parametrize("bound", [1, 0])
+def test_filter_signed_far_disparities(engine, monkeypatch, bound):
+    # negative and far disparities (|d| up to 300 on a 72 x 20 image): the queue
+    # walk's in-image intervals with reversed ends (d < 0) and ends clamped to
+    # int8, candidates with no in-image view at all, every view out of image
+    V, aw, H, W = 32, 8, 20, 72
+    rng = np.random.default_rng(4242 + bound)
+    disp = rng.choice(np.float32([-300.0, -40.0, -7.5, -2.0, -0.5, 0.5, 2.0, 7.5, 40.0, 300.0]), size=(V, H, W))
+    disp += rng.choice(np.float32([0.0, 0.25, 0.5]), size=(V, H, W))
+    disp[rng.random(disp.shape) < 0.15] = 0.0
+    monkeypatch.setenv("MVS_FILTER_KERNEL", "q")
+    monkeypatch.setenv("MVS_FILTER_BOUND", str(bound))
+    proj, out = engine.filter(dev(disp), aw, 1.0359, 1.0)
+    oproj, oout = orc.filt(disp, aw, 1.0359, 1.0)
+    assert_bits(proj.cpu().numpy(), oproj, "filter projection")
+    assert_bits(out.cpu().numpy(), oout, f"filter output (signed far disparities, bound {bound})")
+
+
 @pytest.mark.parametrize("fb,ns", [(2, 2), (4, 1)])
 def test_filter_ragged_grid(engine, monkeypatch, fb, ns):
     # V = 27 views on rows of aw = 6 (the last camera row holds 3): the queue

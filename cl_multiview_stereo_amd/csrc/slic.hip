@@ -16,19 +16,22 @@ namespace {
 
 // mvs_powrf(x, third) (third = (float)(1/3): the definition's exp(third * log x)
 // in double, rounded to float) for x in rgb2lab's range (0.008856, 1.09]
-// without the double exp/log.  A = cbrt(x) (hardware log2/exp2 estimate, two
-// Newton steps in double) * x^(third - 1/3), the last factor as
-// 1 + delta ln x.  A and the definition's double both lie within ~1e-15
-// (relative) of x^third, so when A(1 -+ 1e-12) round to the same float the
-// definition rounds to it too (rounding is monotone); otherwise (about 2 in
-// 10^5 inputs) the definition itself is evaluated.  Checked on every 8-bit
-// RGB colour against the oracle (tests/test_gpu_parity.py).
+// without the double exp/log.  A = cbrt(x) (hardware log2/exp2 estimate, one
+// Newton step in double) * x^(third - 1/3), the last factor as
+// 1 + delta ln x.  The estimate's relative error e0 (~2^-22: two 1-ulp
+// hardware ops) becomes e0^2 plus the rounding of the float residual and
+// reciprocal (~2^-45 each), together below ~3e-13; the definition's double
+// lies within ~1e-15 of x^third.  So when A(1 -+ 1e-12) round to the same
+// float the definition rounds to it too (rounding is monotone); otherwise
+// (about 2 in 10^5 inputs) the definition itself is evaluated.  Checked on
+// every 8-bit RGB colour -- the kernel's whole input domain -- against the
+// oracle (tests/test_gpu_parity.py).  (A second Newton step, the round-4
+// form, cost ~25 % of k_cvt's VALU for error the check does not need.)
 __device__ __forceinline__ float powr_third(float x) {
   const float l2 = __builtin_amdgcn_logf(x);  // log2 x, v_log_f32
   const double xd = (double)x;
   double c = (double)__builtin_amdgcn_exp2f(l2 * (1.0f / 3.0f));
-#pragma unroll
-  for (int i = 0; i < 2; i++) {  // Newton on c^3 = x; the correction's own error is below 1e-7 of it
+  {  // Newton on c^3 = x; the correction's own error is below 1e-7 of it
     const double c2 = c * c;
     const float res = (float)fma(c2, c, -xd);
     c = c - (double)(res * __builtin_amdgcn_rcpf((float)(3.0 * c2)));

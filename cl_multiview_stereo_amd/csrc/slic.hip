@@ -16,30 +16,32 @@ namespace {
 
 // mvs_powrf(x, third) (third = (float)(1/3): the definition's exp(third * log x)
 // in double, rounded to float) for x in rgb2lab's range (0.008856, 1.09]
-// without the double exp/log.  A = cbrt(x) (hardware log2/exp2 estimate, one
-// Newton step in double) * x^(third - 1/3), the last factor as
-// 1 + delta ln x.  The estimate's relative error e0 (~2^-22: two 1-ulp
-// hardware ops) becomes e0^2 plus the rounding of the float residual and
-// reciprocal (~2^-45 each), together below ~3e-13; the definition's double
-// lies within ~1e-15 of x^third.  So when A(1 -+ 1e-12) round to the same
-// float the definition rounds to it too (rounding is monotone); otherwise
-// (about 2 in 10^5 inputs) the definition itself is evaluated.  Checked on
-// every 8-bit RGB colour -- the kernel's whole input domain -- against the
-// oracle (tests/test_gpu_parity.py).  (A second Newton step, the round-4
-// form, cost ~25 % of k_cvt's VALU for error the check does not need.)
+// without double arithmetic.  A = cbrt(x) * x^(third - 1/3) as an unevaluated
+// float sum c + lo: c the hardware log2/exp2 estimate (relative error e0 ~
+// 2^-22, two 1-ulp ops), lo = c (delta ln x) - (one Newton correction).  The
+// correction's residual c^3 - x is formed exactly enough with FMAs (c^2 =
+// p + pe exactly; p c - x rounded once, ~2^-44 x), so A's error is e0^2 plus
+// the residual's and the reciprocal's roundings, together ~1.2e-13; the
+// definition's double lies within ~1e-15 of x^third.  The float sums
+// c + (lo -+ 1e-12 c) round A(1 -+ 1e-12) once each (their inner roundings
+// move the ends by ~3e-14 c), so when they agree the definition rounds to
+// the same float (rounding is monotone); otherwise (about 2 in 10^5 inputs)
+// the definition itself is evaluated.  Checked on every 8-bit RGB colour --
+// the kernel's whole input domain -- against the oracle
+// (tests/test_gpu_parity.py).  (Round 4 formed A in double with two Newton
+// steps: ~half of k_cvt's VALU.)
 __device__ __forceinline__ float powr_third(float x) {
   const float l2 = __builtin_amdgcn_logf(x);  // log2 x, v_log_f32
-  const double xd = (double)x;
-  double c = (double)__builtin_amdgcn_exp2f(l2 * (1.0f / 3.0f));
-  {  // Newton on c^3 = x; the correction's own error is below 1e-7 of it
-    const double c2 = c * c;
-    const float res = (float)fma(c2, c, -xd);
-    c = c - (double)(res * __builtin_amdgcn_rcpf((float)(3.0 * c2)));
-  }
-  const double delta = (double)(1.0f / 3.0f) - 1.0 / 3.0;  // 9.934e-9
-  const double a = fma(c, delta * (double)(l2 * 0.693147182f), c);
-  const float lo = (float)(a * (1.0 - 1e-12)), hi = (float)(a * (1.0 + 1e-12));
-  return lo == hi ? lo : mvs_powrf(x, 1.0f / 3.0f);
+  const float c = __builtin_amdgcn_exp2f(l2 * (1.0f / 3.0f));
+  const float p = c * c;
+  const float pe = fmaf(c, c, -p);                   // c^2 = p + pe
+  const float r = fmaf(pe, c, fmaf(p, c, -x));       // c^3 - x
+  const float dlt = r * __builtin_amdgcn_rcpf(3.0f * p);  // Newton: cbrt(x) = c - dlt
+  constexpr float kDelta = (float)((double)(1.0f / 3.0f) - 1.0 / 3.0);  // 9.934e-9
+  const float lo = fmaf(c, kDelta * (l2 * 0.693147182f), -dlt);     // A = c + lo
+  const float m = 1e-12f * c;
+  const float a0 = c + (lo - m), a1 = c + (lo + m);
+  return a0 == a1 ? a0 : mvs_powrf(x, 1.0f / 3.0f);
 }
 
 // ---- rgb2lab + cvt, clcode.cl:21-59, 125-151 (s0 read as blue) -----------

@@ -44,6 +44,16 @@ __device__ __forceinline__ float powr_third(float x) {
   return a0 == a1 ? a0 : mvs_powrf(x, 1.0f / 3.0f);
 }
 
+// x / c for rgb2lab's constant divisors: q = x RN(1/c), its remainder by one
+// FMA and one FMA correction -- the IEEE quotient for every operand rgb2lab
+// forms (all 2^24 colours checked against the oracle's divisions,
+// tests/test_gpu_parity.py test_cvt_every_rgb_colour), in 3 VALU instead of
+// the ~10 of the general IEEE divide sequence
+__device__ __forceinline__ float div_by(float x, float c, float rc) {
+  const float q = x * rc;
+  return fmaf(fmaf(-q, c, x), rc, q);
+}
+
 // ---- rgb2lab + cvt, clcode.cl:21-59, 125-151 (s0 read as blue) -----------
 __device__ __forceinline__ float4 rgb2lab(uint32_t px) {
   float _b = (float)(px & 0xffu) * 0.0039216f;
@@ -53,12 +63,12 @@ __device__ __forceinline__ float4 rgb2lab(uint32_t px) {
   float y = _r * 0.212671f + _g * 0.715160f + _b * 0.072169f;
   float z = _r * 0.019334f + _g * 0.119193f + _b * 0.950227f;
   const float epsilon = 0.008856f, kappa = 903.3f;
-  float xr = x / 0.950456f, yr = y / 1.0f, zr = z / 1.088754f;
+  float xr = div_by(x, 0.950456f, 1.0f / 0.950456f), yr = y, zr = div_by(z, 1.088754f, 1.0f / 1.088754f);
   const float third = 1.0f / 3.0f;
   (void)third;  // powr_third(v) == mvs_powrf(v, third)
-  float fx = xr > epsilon ? powr_third(xr) : (kappa * xr + 16.0f) / 116.0f;
-  float fy = yr > epsilon ? powr_third(yr) : (kappa * yr + 16.0f) / 116.0f;
-  float fz = zr > epsilon ? powr_third(zr) : (kappa * zr + 16.0f) / 116.0f;
+  float fx = xr > epsilon ? powr_third(xr) : div_by(kappa * xr + 16.0f, 116.0f, 1.0f / 116.0f);
+  float fy = yr > epsilon ? powr_third(yr) : div_by(kappa * yr + 16.0f, 116.0f, 1.0f / 116.0f);
+  float fz = zr > epsilon ? powr_third(zr) : div_by(kappa * zr + 16.0f, 116.0f, 1.0f / 116.0f);
   return make_float4(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz), 0.0f);
 }
 

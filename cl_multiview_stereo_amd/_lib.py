@@ -18,7 +18,7 @@ EXPORTS = [
     "mvs_cvt_d", "mvs_slic_d", "mvs_grid_d", "mvs_boundary_d", "mvs_sweep_spixl_d", "mvs_sweep_pixel_sad_d",
     "mvs_box_stats_d", "mvs_ncc_volume_d", "mvs_wta_d", "mvs_ncc_wta_d", "mvs_ncc_wta_range_d", "mvs_flatness_d", "mvs_init_state_d",
     "mvs_propagate_d", "mvs_spixl_to_image_d", "mvs_refine_d", "mvs_filter_d",
-    "mvs_box_stats_range_d", "mvs_set_ncc_variant", "mvs_ncc_last_variant", "mvs_set_kernel_timing", "mvs_kernel_times", "mvs_init_state_range_d",
+    "mvs_box_stats_range_d", "mvs_set_ncc_variant", "mvs_ncc_last_variant", "mvs_ncc_last_variant_n", "mvs_set_kernel_timing", "mvs_kernel_times", "mvs_init_state_range_d",
     "mvs_proj_inv_d", "mvs_remove_inconsistency_d", "mvs_proj_inv_rows_d", "mvs_remove_inconsistency_rows_d",
     "mvs_do_super_pixel_seg", "mvs_do_initial_depth_estimation", "mvs_do_refinement", "mvs_do_consistency_filter",
     "mvs_init_state_range_l16_d", "mvs_propagate_l16_d", "mvs_spixl_to_image_l16_d",

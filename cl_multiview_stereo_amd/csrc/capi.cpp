@@ -153,7 +153,7 @@ void* scratch(mvs_ctx* ctx, size_t bytes, int* rc) {
 extern "C" {
 
 const char* mvs_last_error(void) { return g_err.c_str(); }
-const char* mvs_version(void) { return "mvs-mi355x 0.6 (gfx950)"; }
+const char* mvs_version(void) { return "mvs-mi355x 0.7 (gfx950)"; }
 
 int mvs_create(int device, mvs_ctx** out) {
   if (!out) return mvs::arg_fail("mvs_create: out is null");
@@ -339,21 +339,31 @@ int mvs_set_kernel_timing(mvs_ctx* c, int on) {
 int mvs_kernel_times(mvs_ctx* c, float* ms, int cap, int* n) {
   if (!c || !n || (cap > 0 && !ms)) return mvs::arg_fail("mvs_kernel_times: bad arguments");
   const int k = (int)c->kev_used;
-  for (int i = 0; i < k && i < cap; i++) {
+  *n = k;
+  // more launches than the caller's buffer holds: fail and keep the record
+  // (a truncated list divided by every swept view would read low)
+  if (k > cap) return mvs::arg_fail("mvs_kernel_times: more launches recorded than cap");
+  for (int i = 0; i < k; i++) {
     MVS_HIP(hipEventSynchronize(c->kev[i].second), "hipEventSynchronize(kernel timing)");
     float t = 0.0f;
     MVS_HIP(hipEventElapsedTime(&t, c->kev[i].first, c->kev[i].second), "hipEventElapsedTime(kernel timing)");
     ms[i] = t;
   }
-  *n = k;
   c->kev_used = 0;
   return 0;
 }
 
-int mvs_ncc_last_variant(mvs_ctx* c, int32_t* out8) {
-  if (!c || !out8) return mvs::arg_fail("mvs_ncc_last_variant: null argument");
-  for (int i = 0; i < 8; i++) out8[i] = c->ncc_last[i];
+int mvs_ncc_last_variant(mvs_ctx* c, int32_t* out7) {
+  if (!c || !out7) return mvs::arg_fail("mvs_ncc_last_variant: null argument");
+  for (int i = 0; i < 7; i++) out7[i] = c->ncc_last[i];  // the 0.5 report: seven slots, as its callers size it
   return 0;
+}
+
+int mvs_ncc_last_variant_n(mvs_ctx* c, int32_t* out, int cap) {
+  if (!c || (cap > 0 && !out) || cap < 0) return mvs::arg_fail("mvs_ncc_last_variant_n: bad arguments");
+  const int k = cap < 8 ? cap : 8;
+  for (int i = 0; i < k; i++) out[i] = c->ncc_last[i];
+  return 8;
 }
 
 int mvs_ncc_volume_d(mvs_ctx* c, int W, int H, const uint8_t* l8, const int32_t* box, const mvs_array* a, int K,

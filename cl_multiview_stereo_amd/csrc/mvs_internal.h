@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -48,10 +49,30 @@ inline std::pair<hipEvent_t, hipEvent_t> kernel_events(mvs_ctx* ctx) {
   if (!ctx->ktime) return {nullptr, nullptr};
   if (ctx->kev_used == ctx->kev.size()) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return {nullptr, nullptr};
+    if (hipEventCreate(&a) != hipSuccess) return {nullptr, nullptr};
+    if (hipEventCreate(&b) != hipSuccess) {
+      hipEventDestroy(a);
+      return {nullptr, nullptr};
+    }
     ctx->kev.push_back({a, b});
   }
   return ctx->kev[ctx->kev_used++];
+}
+
+// Raise kern's dynamic-LDS limit to lds bytes on ctx's device when above the
+// 64 KB default.  HIP keeps the attribute per device, so the raise is cached
+// per (kernel, device) -- a context on a second GPU raises it there too --
+// under a mutex (contexts may launch from several host threads).
+inline hipError_t raise_lds(mvs_ctx* ctx, const void* kern, size_t lds) {
+  if (lds <= 64 * 1024) return hipSuccess;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> done;
+  std::lock_guard<std::mutex> lock(mu);
+  size_t& have = done[{kern, ctx->device}];
+  if (lds <= have) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) have = lds;
+  return e;
 }
 
 void set_error(const std::string& msg);

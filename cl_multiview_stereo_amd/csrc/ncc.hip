@@ -612,13 +612,7 @@ int launch_ncc_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccRe
   dim3 g(8 * a.tiles_per_xcd);
   auto kern = vol ? k_ncc_volume<K, TH, DPW, NW, BW, PAR, false, NB> : k_ncc_volume<K, TH, DPW, NW, BW, PAR, true, NB>;
   if (!vol) lds = std::max(lds, (size_t)3 * 4 * NW * TH * 64) + 4 * TH * 64;  // WTA partials; + s_r [64][TH]
-  // per instantiation and form (volume / fused): raise the limit once, not on every launch
-  static size_t lds_set[2] = {64 * 1024, 64 * 1024};
-  if (lds > lds_set[vol ? 0 : 1]) {
-    MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-            "hipFuncSetAttribute(ncc lds)");
-    lds_set[vol ? 0 : 1] = lds;
-  }
+  MVS_HIP(raise_lds(ctx, (const void*)kern, lds), "hipFuncSetAttribute(ncc lds)");
   const auto ev = vol ? std::pair<hipEvent_t, hipEvent_t>{nullptr, nullptr} : kernel_events(ctx);  // (the fused sweep only)
   hipExtLaunchKernelGGL(kern, g, dim3(NW * 64), lds, s, ev.first, ev.second, 0, stats, pk, plan, a, vol, wo);
   MVS_LAUNCH_CHECK(vol ? "k_ncc_volume" : "k_ncc_volume (fused WTA)");
@@ -811,7 +805,11 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
     }
     if (mf_on && horiz && nn > 0) {
       mplan[r] = make_plan_mfma(levels_host, D, nn, fdx, fdy, bl, 2);
-      if (mplan[r].band_w <= 192) {
+      // the run keeps every step's level offsets in LDS (tmax = chunks x
+      // neighbours): past the 160 KB of a CU (large D with many neighbours)
+      // the scalar kernels take the view
+      const int tm = ((D + 31) / 32) * nn;
+      if (mplan[r].band_w <= 192 && mfma_lds_bytes(mplan[r], mplan[r].band_w, 2, tm, D) <= (size_t)160 * 1024) {
         mf[r] = 1;
         continue;
       }
@@ -856,13 +854,14 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
       std::vector<int32_t> table;
       NccPlanM run;  // the run's band extents (LDS check)
       run.ndb = ndb;
+      run.vert = vert;
       while (j < n && mf[j] && j - i < maxrun && mplan[j].vert == vert && mplan[j].ndb == ndb && mnb[j] == nb) {
         const int z = z0 + j;
         run.pk_pairs = std::max(run.pk_pairs, mplan[j].pk_pairs);
         run.st_pairs = std::max(run.st_pairs, mplan[j].st_pairs);
         const int bw2 = std::max(bw, mplan[j].band_w);
         const int tm2 = std::max(tmax, ((D + 16 * ndb - 1) / (16 * ndb)) * sn_host[z]);
-        if (vert && j > i && mfma_lds_bytes(run, bw2, nb, tm2, D) > 80 * 1024) break;
+        if (j > i && mfma_lds_bytes(run, bw2, nb, tm2, D) > (size_t)(vert ? 80 : 160) * 1024) break;
         bw = bw2;
         tmax = tm2;
         a.z[j - i] = z;

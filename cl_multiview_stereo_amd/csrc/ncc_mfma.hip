@@ -479,12 +479,7 @@ int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccM
   const size_t lds = std::max((size_t)NB * 16 * (a.pk_pairs + a.st_pairs) * (BW + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
                      2 * 64 * TH * 4 + (size_t)tmax * DC * 2;
   auto kern = k_ncc_mfma<BW, TAIL, VERT, NDB, NB, DBG>;
-  static size_t lds_set = 64 * 1024;  // per instantiation: raise the limit once, not on every launch
-  if (lds > lds_set) {
-    MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-            "hipFuncSetAttribute(ncc mfma lds)");
-    lds_set = lds;
-  }
+  MVS_HIP(raise_lds(ctx, (const void*)kern, lds), "hipFuncSetAttribute(ncc mfma lds)");
   const auto ev = kernel_events(ctx);  // (timing off: plain launch)
   hipExtLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(512), lds, ctx->stream, ev.first, ev.second, 0, stats, pk,
                         plan, a, wo);
@@ -557,7 +552,9 @@ NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, co
 }
 
 size_t mfma_lds_bytes(const NccPlanM& p, int band_w, int nb, int tmax, int D) {
-  const int bwt = vert_bw(band_w, D % (16 * p.ndb) != 0);
+  const bool tail = D % (16 * p.ndb) != 0;
+  // the band pitch template launch_ncc_mfma picks: VERT by vert_bw, horizontal 128 | 192
+  const int bwt = p.vert ? vert_bw(band_w, tail) : (tail || band_w > 128 ? 192 : 128);
   return std::max((size_t)nb * 16 * (p.pk_pairs + p.st_pairs) * (bwt + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
          2 * 64 * 8 * 4 + (size_t)tmax * 16 * p.ndb * 2;
 }

@@ -1253,9 +1253,7 @@ int launch_sad_band_t(mvs_ctx* ctx, int V, int W, int H, const float* lab, const
   a.tiles_per_xcd = (a.ntiles + 7) / 8;
   auto kern = k_sad_band<TH, PPW>;
   if (aff) kern = a.bw == 64 ? k_sad_band<TH, PPW, true, 64> : k_sad_band<TH, PPW, true, 128>;
-  if (lds > 64 * 1024)
-    MVS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-            "hipFuncSetAttribute(sad lds)");
+  MVS_HIP(raise_lds(ctx, (const void*)kern, lds), "hipFuncSetAttribute(sad lds)");
   hipLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(256), lds, ctx->stream, (const float4*)lab,
                      ctx->d_levels, (const SadRec*)dev, a, disp);
   MVS_LAUNCH_CHECK("k_sad_band");

@@ -232,15 +232,19 @@ class Engine:
         """The recorded fused-sweep launches' kernel times in ms (waits for them; starts a new record)."""
         buf = (C.c_float * cap)()
         n = C.c_int(0)
-        _lib.check(self.L.mvs_kernel_times(self.ctx, buf, cap, C.byref(n)), "mvs_kernel_times")
-        return list(buf[:min(n.value, cap)])
+        rc = self.L.mvs_kernel_times(self.ctx, buf, cap, C.byref(n))
+        if rc != 0 and n.value > cap:
+            return self.kernel_times(n.value)  # the record is kept: read it whole
+        _lib.check(rc, "mvs_kernel_times")
+        return list(buf[:n.value])
 
     def ncc_last_variant(self) -> dict:
         """The last NCC launch: K, tile rows, levels per wave, waves, band width,
         PAR (row parity: 0 mixed, 1 every band row pair-aligned, 2 odd pk / even
         stats rows), FUSE, NB (band buffers: 1 single, 2 double)."""
         v = (C.c_int32 * 8)()
-        _lib.check(self.L.mvs_ncc_last_variant(self.ctx, v), "mvs_ncc_last_variant")
+        if self.L.mvs_ncc_last_variant_n(self.ctx, v, 8) != 8:
+            raise _lib.MvsError("mvs_ncc_last_variant_n: unexpected slot count")
         return dict(zip(("K", "TH", "DPW", "NW", "BW", "PAR", "FUSE", "NB"), list(v)))
 
     def ncc_volume(self, l8, box, cam: CameraArray, z: int, K: int = 5, out=None):

@@ -140,10 +140,10 @@ class Pipeline:
     extents, superpixel sweep: latency/L2-bound gathers) runs on a second HIP
     stream with its own libmvs context, beside the per-pixel chain (window
     planes, fused NCC sweep + WTA) on the caller's stream; the caller's stream
-    joins the side stream before refinement.  bench.py makes it the default
-    for the unsharded fused-NCC configurations (--serial turns it off); the
-    class default stays False so library callers get one stream unless they
-    ask for the second."""
+    joins the side stream before refinement.  One stream is the default here
+    and in bench.py (round 5: with the matrix-core sweep the side stream
+    measured no gain); `bench.py --concurrent` runs the headline
+    with it, and the default line reports it as `concurrent_variant`."""
 
     def __init__(self, engine: Engine, settings: params.Settings, W: int, H: int,
                  view_subset: list[list[int]] | None = None, pixel_cost: str | None = "ncc",

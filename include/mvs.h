@@ -183,17 +183,22 @@ int mvs_ncc_wta_range_d(mvs_ctx* ctx, int W, int H, const uint8_t* l8, const int
  * on a pair.  Variants that do not fit the LDS fall back as in the default
  * chain.  mvs_ncc_last_variant reports the last launch as
  * {K, TH, levels per wave, waves, band width, row parity (0 mixed, 1 every band
- * row pair-aligned, 2 every pk row odd and stats row even), fused, band buffers
- * (1 single-buffered, 2 double-buffered)}: eight int32. */
+ * row pair-aligned, 2 every pk row odd and stats row even), fused}: seven
+ * int32 (the 0.5 report).  mvs_ncc_last_variant_n (0.7) writes the first
+ * min(cap, 8) of those eight -- the eighth: band buffers (1 single-buffered,
+ * 2 double-buffered) -- and returns 8, the slots it has. */
 int mvs_set_ncc_variant(mvs_ctx* ctx, int waves, int levels_per_wave, int band_w, int general_rows);
-int mvs_ncc_last_variant(mvs_ctx* ctx, int32_t* out8);
+int mvs_ncc_last_variant(mvs_ctx* ctx, int32_t* out7);
+int mvs_ncc_last_variant_n(mvs_ctx* ctx, int32_t* out, int cap);
 /* Kernel timing (a measurement aid, no reference counterpart): with timing on,
  * every fused NCC sweep launch (mvs_ncc_wta_d / mvs_ncc_wta_range_d) records
  * start / stop events of its own dispatch (hipExtLaunchKernel), so the time is
  * the kernel's alone -- an event recorded on the stream before a call can fire
  * while the previous kernel is still running.  mvs_kernel_times waits for the
- * recorded launches and returns their times in ms (up to cap of them; *n = how
- * many were recorded), then starts a new record; switching timing on also does. */
+ * recorded launches and returns their times in ms (*n = how many were
+ * recorded), then starts a new record; switching timing on also does.  When
+ * more launches were recorded than cap it fails (MVS_E_ARG) with *n set and the
+ * record kept, so the caller can retry with a buffer of *n. */
 int mvs_set_kernel_timing(mvs_ctx* ctx, int on);
 int mvs_kernel_times(mvs_ctx* ctx, float* ms, int cap, int* n);
 

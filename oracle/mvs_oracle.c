@@ -557,6 +557,57 @@ void orc_ncc_volume(int V, int W, int H, const uint8_t* q, const float* levels, 
     }
 }
 
+/* Accuracy yardstick for the i8 definition above (CPU
+ * only, never a parity target): the same NCC cost on the float L plane itself
+ * (lab[.][0], no 8-bit quantisation), window sums and the correlation in
+ * double.  Same windows, validity, shifts, neighbour maximum and 1 - max(-1, .)
+ * conventions: a textureless reference window costs 1 (any neighbour valid), a
+ * textureless neighbour window contributes 0, no valid neighbour window 2. */
+void orc_ncc_volume_f32(int V, int W, int H, const float* lab, const float* levels, int D, const int* vs,
+                        const int* sn, int aw, float bl, int K, int z, float* vol) {
+  int r = K / 2, nk = K * K;
+  long P = (long)W * H;
+  int rx = z % aw, ry = z / aw;
+#pragma omp parallel for schedule(static)
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      int rin = (x - r >= 0 && x + r < W && y - r >= 0 && y + r < H);
+      double Sr = 0.0, Srr = 0.0;
+      if (rin)
+        for (int j = -r; j <= r; j++)
+          for (int i = -r; i <= r; i++) {
+            double a = lab[4 * (z * P + (long)(y + j) * W + x + i)];
+            Sr += a; Srr += a * a;
+          }
+      double vr = nk * Srr - Sr * Sr;
+      for (int dl = 0; dl < D; dl++) {
+        float d = levels[dl];
+        double best = -INFINITY;
+        for (int n = 0; n < sn[z]; n++) {
+          int view = vs[V * z + n];
+          int dx = view % aw - rx, dy = view / aw - ry;
+          int tx = (int)roundf(d * (float)dx);
+          int ty = (int)roundf((bl * d) * (float)dy);
+          int px = x - tx, py = y - ty;
+          if (!rin || px - r < 0 || px + r >= W || py - r < 0 || py + r >= H) continue;
+          double Sp = 0.0, Spp = 0.0, Srp = 0.0;
+          for (int j = -r; j <= r; j++)
+            for (int i = -r; i <= r; i++) {
+              double a = lab[4 * (z * P + (long)(y + j) * W + x + i)];
+              double b = lab[4 * ((long)view * P + (long)(py + j) * W + px + i)];
+              Sp += b; Spp += b * b; Srp += a * b;
+            }
+          double vp = nk * Spp - Sp * Sp;
+          double e = (vr > 1e-9 && vp > 1e-9) ? (nk * Srp - Sr * Sp) / sqrt(vr * vp) : 0.0;
+          if (e > best) best = e;
+        }
+        double E = best;
+        if (!(E > -1.0)) E = -1.0;
+        vol[((long)dl * H + y) * W + x] = (float)(1.0 - E);
+      }
+    }
+}
+
 /* Build-defined WTA over a cost volume [D][H][W]: first minimum (strict <,
  * init 1e6, disparity levels[0]-less default 0), confidence = c2 - c1 where
  * c2 = min cost over levels outside {best-1, best, best+1} (0 if none). */

@@ -193,6 +193,20 @@ def ncc_volume(l8_all, levels, view_subset, subset_num, array_width, bl_ratio, K
     return vol
 
 
+def ncc_volume_f32(lab_all, levels, view_subset, subset_num, array_width, bl_ratio, K, z):
+    """The NCC cost on the float L plane (no 8-bit quantisation, double sums):
+    the accuracy yardstick of the i8 definition (scripts/ncc_i8_vs_f32.py)."""
+    lab = np.ascontiguousarray(lab_all, np.float32)
+    levels = np.ascontiguousarray(levels, np.float32)
+    vs = np.ascontiguousarray(view_subset, np.int32)
+    sn = np.ascontiguousarray(subset_num, np.int32)
+    V, H, W = lab.shape[:3]
+    vol = np.zeros((len(levels), H, W), np.float32)
+    lib().orc_ncc_volume_f32(V, W, H, _p(lab, f32p), _p(levels, f32p), len(levels), _p(vs, i32p), _p(sn, i32p),
+                             array_width, _f(bl_ratio), K, z, _p(vol, f32p))
+    return vol
+
+
 def wta(vol, levels):
     vol = np.ascontiguousarray(vol, np.float32)
     levels = np.ascontiguousarray(levels, np.float32)

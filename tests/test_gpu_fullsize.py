@@ -5,7 +5,9 @@ checked only on crops before round 5 ("What's missing" 1):
   refinement (5 propagations, kernel_size 1080) + cross-view consistency
   filter -- through the product Pipeline exactly as `bench.py --config c3`
   runs it (fused sweep, superpixel chain on the side stream).  Labels, the
-  superpixel seeds, the refined and the filtered maps are compared bit for bit
+  superpixel seeds, the per-pixel NCC disparity and confidence of every view
+  (the headline kernel, k_ncc_mfma, at full size), the refined and the
+  filtered maps are compared bit for bit
   with the oracle's full-size run (clcode.cl:1076-1931 refinement,
   :1995-2101 projection + removal; pipeline.cpp:162-175 order).
 * C5 -- 5 views 4096x3072, SLIC S = 40 (the incomplete 16x16-tile update
@@ -63,6 +65,15 @@ def test_c3_full_size(engine, concurrent):
     _bits(out.labels.cpu().numpy().view(np.uint32), lb, "SLIC labels (5 views, S = 32)")
     _bits(out.spixl.cpu().numpy(), sp, "superpixel seeds after the sweep")
     _bits(out.rep.cpu().numpy(), rep, "superpixel extents")
+    # the per-pixel depth map (the headline's fused NCC 5x5 x 128 sweep + WTA,
+    # k_ncc_mfma at 1920x1080, every reference view) and its confidence, against
+    # the oracle's fused definition: orc_ncc_volume + orc_wta per view
+    cam = p.cam
+    q = orc.l8(lab)
+    for z in range(aw):
+        od, oc = orc.wta(orc.ncc_volume(q, cam.levels, cam.view_subset, cam.subset_num, aw, 1.0, 5, z), cam.levels)
+        _bits(out.disp[z].cpu().numpy(), od, f"per-pixel NCC disparity, view {z}, 1920x1080")
+        _bits(out.conf[z].cpu().numpy(), oc, f"per-pixel NCC confidence, view {z}, 1920x1080")
     ref = orc.refine(sp, lb, rep, p.cam.view_subset, p.cam.subset_num, aw, 1.0, S, kernel_size=st.kernel_size,
                      kernel_step=st.kernel_step)
     _bits(out.disp_refined.cpu().numpy(), ref["disp"], "refined (fused) disparity, 5 views 1920x1080")

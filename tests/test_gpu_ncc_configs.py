@@ -377,3 +377,29 @@ def test_box_planes(engine, K, W, H):
     got_pk = box[1].reshape(-1).view(np.uint8).reshape(3, Hp // 2, W, 16)
     same(got_st, st, f"stats K{K} {W}x{H}")
     assert np.array_equal(got_pk, pk), f"packed rows K{K} {W}x{H}"
+
+
+@pytest.mark.parametrize("D,nn", [(1600, 16), (3200, 16)])
+def test_fused_large_d_horizontal(eng, D, nn):
+    """A horizontal list whose matrix-core run would not fit the LDS (ADVICE
+    r05): 16 horizontal neighbours (a 17x1 array, 8 views either side) and
+    fractional levels 0.05 apart, so every 32-level chunk's band stays within
+    the 192-column pitch.  k_ncc_mfma keeps a run's level offsets in LDS
+    (chunks x neighbours x 64 B): at D = 1600 they fit and the matrix-core
+    form runs (DPW >= 16 in the report); at D = 3200 they would pass 160 KB and
+    the scalar fused kernel takes the view.  Both bit-exact against the oracle."""
+    aw, W, H, z = 17, 72, 12, 8
+    levels = (np.arange(D, dtype=np.float32) * np.float32(0.05)).astype(np.float32)
+    vs, sn = params.flatten_subsets(params.neighbour_lists(aw, 1, nn // 2, 0))
+    cam = CameraArray(aw, 1.0, levels, vs, sn)
+    assert int(cam.subset_num[z]) == nn
+    stack, _ = synth.make_stack(W, H, aw, 1, 0, 3, 1.0, 0xD0 + D)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    box = eng.box_stats(l8, 5)
+    want = orc.ncc_volume(l8.cpu().numpy(), cam.levels, cam.view_subset, cam.subset_num, aw, 1.0, 5, z)
+    od, oc = orc.wta(want, cam.levels)
+    fd, fc = eng.ncc_wta(l8, box, cam, z, 5)
+    v = eng.ncc_last_variant()
+    assert v["FUSE"] == 1 and (v["DPW"] >= 16) == (D == 1600), v  # DPW >= 16: the matrix-core form
+    same(fd, od, f"fused disp D{D}")
+    same(fc, oc, f"fused conf D{D}")

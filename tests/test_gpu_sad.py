@@ -43,6 +43,29 @@ def test_sad_c2_band(engine, z):
     _check(engine, stack, _cam(5, 1, 0, 127, 4, 0, 1.0), z, z + 1, f"c2 band z{z}")
 
 
+def test_sad_c2_full_height_bands(engine):
+    """C2 itself (5 views 1920x1080, levels 0..127, the bench's stack): the
+    GPU sweeps every whole view; the oracle recomputes three 62-row bands of
+    each -- the top, the middle tile rows and the bottom rows of the 1080-row
+    image -- from the band's Lab rows plus the window's 2-row margin (with
+    horizontal-only neighbours a row's taps stay within rows y-2..y+2, so the
+    band's inner rows are exactly the full image's)."""
+    W, H, R = 1920, 1080, 2
+    stack, _ = synth.make_stack(W, H, 5, 1, 0, 127, 1.0, 0x5EED + 2)  # = bench.py's C2 stack
+    cam = _cam(5, 1, 0, 127, 4, 0, 1.0)
+    lab, _ = engine.cvt(torch.from_numpy(stack).cuda())
+    got = engine.sweep_pixel_sad(lab, cam, 0, 5).cpu().numpy()
+    labh = lab.cpu().numpy()
+    for y0 in (0, H // 2 - 31, H - 62):
+        y1 = y0 + 62
+        b0, b1 = max(0, y0 - R), min(H, y1 + R)
+        want = orc.sweep_pixel_sad(np.ascontiguousarray(labh[:, b0:b1]), cam.levels, cam.view_subset, cam.subset_num,
+                                   cam.array_width, cam.bl_ratio)[:, y0 - b0:y1 - b0]
+        g = got[:, y0:y1]
+        bad = np.count_nonzero(g.view(np.uint32) != want.view(np.uint32))
+        assert bad == 0, f"rows {y0}..{y1 - 1}: {bad}/{g.size} disparities differ"
+
+
 def test_sad_reference_defaults_geometry(engine):
     """The reference's own 3x3 array with bl_ratio 1.0359 (fractional vertical
     shifts, per-row truncation), levels 30..60, every view."""

@@ -781,10 +781,13 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   // lists take the matrix-core form only with MVS_NCC_MFMA_V=1 (that choice)
   // or 22 | 21 | 12 | 11 (chunk blocks, buffers: that form): C4's tall bands
   // keep it DMA-bound and slower than the scalar kernels
+  // K = 7 (C5): horizontal lists in 16-level chunks (its 2 x 8-pixel blocks'
+  // operands take 32 VGPRs); MVS_NCC_MFMA7=0 keeps the scalar kernels (A/B)
   const char* mfe = getenv("MVS_NCC_MFMA");
   const char* mfv = getenv("MVS_NCC_MFMA_V");
-  const bool mf_on = !vol && K == 5 && !(mfe && atoi(mfe) == 0) && !ctx->ncc_nw && !ctx->ncc_dpw && !ctx->ncc_general &&
-                     !ctx->ncc_bw;
+  const char* mf7 = getenv("MVS_NCC_MFMA7");
+  const bool mf_on = !vol && (K == 5 || (K == 7 && !(mf7 && atoi(mf7) == 0))) && !(mfe && atoi(mfe) == 0) &&
+                     !ctx->ncc_nw && !ctx->ncc_dpw && !ctx->ncc_general && !ctx->ncc_bw;
   const int mfv_form = mfv ? atoi(mfv) : 0;  // 0: off, 1: automatic, else the form
   std::vector<char> mf(n, 0);
   std::vector<NccPlanM> mplan(n);
@@ -804,17 +807,18 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
       if (fdy[k] != 0.0f) horiz = false;
     }
     if (mf_on && horiz && nn > 0) {
-      mplan[r] = make_plan_mfma(levels_host, D, nn, fdx, fdy, bl, 2);
+      const int ndb = K == 5 ? 2 : 1;
+      mplan[r] = make_plan_mfma(levels_host, D, nn, fdx, fdy, bl, ndb, K);
       // the run keeps every step's level offsets in LDS (tmax = chunks x
       // neighbours): past the 160 KB of a CU (large D with many neighbours)
       // the scalar kernels take the view
-      const int tm = ((D + 31) / 32) * nn;
+      const int tm = ((D + 16 * ndb - 1) / (16 * ndb)) * nn;
       if (mplan[r].band_w <= 192 && mfma_lds_bytes(mplan[r], mplan[r].band_w, 2, tm, D) <= (size_t)160 * 1024) {
         mf[r] = 1;
         continue;
       }
     }
-    if (mf_on && !horiz && nn > 0 && mfv_form != 0) {
+    if (mf_on && K == 5 && !horiz && nn > 0 && mfv_form != 0) {
       static const int forms[4][2] = {{2, 2}, {2, 1}, {1, 2}, {1, 1}};
       for (const auto& f : forms) {
         const bool forced = mfv_form > 1;
@@ -882,7 +886,7 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
       const int32_t* dev = plan_upload(ctx, table, &rc);
       if (rc) return rc;
       const WtaOut wo{levels_dev, disp + P * i, conf ? conf + P * i : nullptr};
-      rc = launch_ncc_mfma(ctx, stats, pk, dev, a, wo, bw, tmax, vert, ndb, nb);
+      rc = launch_ncc_mfma(ctx, stats, pk, dev, a, wo, bw, tmax, vert, ndb, nb, K);
       if (rc) return rc;
       i = j;
       continue;

@@ -183,11 +183,12 @@ struct NccPlanM {
   int ndb = 2;                   // 16-level blocks per chunk
   bool vert = false;
 };
-NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl, int ndb);
+NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl, int ndb,
+                        int K = 5);
 // the LDS bytes of one workgroup of the matrix-core form
 size_t mfma_lds_bytes(const NccPlanM& p, int band_w, int nb, int tmax, int D);
 int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
-                    const WtaOut& wo, int bw, int tmax, bool vert, int ndb, int nb);
+                    const WtaOut& wo, int bw, int tmax, bool vert, int ndb, int nb, int K);
 
 }  // namespace ncc
 }  // namespace mvs

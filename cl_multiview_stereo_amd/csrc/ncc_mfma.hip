@@ -8,6 +8,10 @@
 
 #include "ncc_common.h"
 
+#ifndef MVS_MFMA_SPLIT
+#define MVS_MFMA_SPLIT 1
+#endif
+
 namespace mvs {
 namespace ncc {
 namespace {
@@ -62,23 +66,32 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int kMfMergeStride = 257;  // LDS merge rows: 256 pixels + 1 (16 classes on distinct banks)
 
 // A tile is 64 columns x 8 rows: a wave owns 8 columns x 8 rows = 4 pixel
-// blocks.  TAIL: D % DC != 0, the last chunk carries dummy levels past the
+// blocks (K = 5: 4 x 4 pixels, one MFMA per level block; K = 7: 2 columns x
+// 8 rows, whose 8-column x 16-row footprint is 8 row pairs = two MFMAs, the
+// second accumulating onto the first).  TAIL: D % DC != 0, the last chunk carries dummy levels past the
 // end.  NDB: 16-level blocks per chunk (DC = 16 NDB levels per step).  NB:
 // band buffers (2: step t+1's bands land while step t computes; 1: staged at
 // the start of each step, the other resident workgroup computing meanwhile).
 // DBG (timing probe only, MVS_NCC_MFMA_DBG): 1 skips the MFMAs and the
 // finish (band DMA, barriers, fold and merge stay), 2 skips the band DMA
-template <int BW, bool TAIL, bool VERT, int NDB, int NB, int DBG = 0>
+template <int K, int BW, bool TAIL, bool VERT, int NDB, int NB, int DBG = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ncc_mfma(
     const uint2* __restrict__ stats, const uint2* __restrict__ pk, const NccMRec* __restrict__ plan, NccArgs a,
     WtaOut wo) {
   static_assert(NDB == 1 || NDB == 2, "one or two 16-level blocks per chunk");
-  static_assert(VERT || (NDB == 2 && NB == 2), "the horizontal form: 32-level chunks, double-buffered");
-  constexpr int R = 2, NW = 8, TH = 8, DC = 16 * NDB, NK = 25, NYB = TH / 4;  // NYB: pixel-block rows
+  static_assert(K == 5 || K == 7, "5 x 5 or 7 x 7 windows");
+  static_assert(K == 5 || !VERT, "K = 7: horizontal lists only");
+  static_assert(VERT || NB == 2, "the horizontal form is double-buffered");
+  static_assert(VERT || NDB == (K == 5 ? 2 : 1), "horizontal chunks: 32 levels (K = 5), 16 (K = 7: A takes 32 VGPRs)");
+  constexpr int R = K / 2, NW = 8, TH = 8, DC = 16 * NDB, NK = K * K;
+  // pixel blocks per wave: XB across (BXW columns each) x NYB down; MF MFMAs per block and level block
+  constexpr int XB = K == 5 ? 2 : 4, NYB = K == 5 ? TH / 4 : 1, NBL = XB * NYB, MF = K == 5 ? 1 : 2;
+  constexpr int BXW = 8 / XB;
   // band row pitch: BW + 1 columns of 16 B, so a lane group's B reads in two
   // rows (row pairs g, g + 1) fall on different banks when the shift per level
   // is even (|dx| = 2: conflict-free instead of 2-way)
   constexpr int BWP = BW + 1;
+  constexpr bool SPLIT = MVS_MFMA_SPLIT;
   extern __shared__ __align__(16) uint8_t smem[];
   const int nbuf = (a.pk_pairs + a.st_pairs) * BWP;  // uint4 per neighbour buffer
   u32x4* nbase = (u32x4*)smem;                      // 2 x {npk[pk_pairs][BW], nst[st_pairs][BW]}
@@ -106,9 +119,42 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   // so wave w stages pk pair row w (w < bhp) and stats pair row w (w < shp),
   // whose clamped row offsets are computed once per tile.  VERT: the rows
   // start at the step's tymax, the waves take the pair rows in turn
-  const int bhp = (TH + 4) / 2, shp = TH / 2;
-  const long pk_row = 2L * W * min(max((y0 - R) / 2 + wave, 0), Hp2 - 1);  // (y0 - R) even: y0 even, R = 2
+  // pk band: K = 5 rows y0 - 2 .. y0 + TH + 1 (pair (y0 - 2) / 2 on); K = 7 the
+  // 8 pairs from (y0 - 4) / 2 (rows y0 - 4 .. y0 + TH + 3: every block's
+  // 16-row footprint, its first and last rows masked off in A)
+  const int bhp = K == 5 ? (TH + 4) / 2 : (TH + 8) / 2, shp = TH / 2;
+  const long pk_row = 2L * W * min(max((y0 >> 1) - (K == 5 ? 1 : 2) + wave, 0), Hp2 - 1);
   const long st_row = 2L * W * min(max(y0 / 2 + wave, 0), Hp2 - 1);
+  // Horizontal lists: a step's scalars (band origin, column span, neighbour
+  // view) are loaded two steps ahead and carried, so no step waits on a
+  // scalar load; its DMA goes through buffer descriptors rebased per step
+  // (base = the neighbour's plane row, 32-bit lane offsets: the clamped
+  // column x 16 B), no per-lane 64-bit address arithmetic.
+  struct StepInfo {
+    int tx, shp, view;  // raw record words: nothing computed on them until they are used
+  };
+  auto load_info = [&](int t, int n) -> StepInfo {
+    const NccMRec& e = rec[t];
+    return StepInfo{e.txmax, e.shp, a.view[ref][n]};
+  };
+  const int lane_x = x0 + lane;
+  auto stage_h = [&](const StepInfo& e, int b) {
+    if (DBG == 2) return;
+    const int span = e.shp >> 16, nblk = (span + 127) >> 6;
+    const long vo = (long)e.view * Pv;
+    u32x4* npk = nbase + b * nbuf;
+    u32x4* nst = npk + a.pk_pairs * BWP;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(pk + vo + pk_row), 0, 16 * W, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(stats + vo + st_row), 0, 16 * W, 0x00020000);
+    for (int cb = 0; cb < nblk; cb++) {
+      const int c0 = min(cb * 64, span);
+      const int voff = 16 * min(max(lane_x - e.tx + c0, 0), W - 1);
+      if (wave < bhp)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (lds_ptr_t)(npk + wave * BWP + c0), 16, voff, 0, 0, 0);
+      if (wave < shp)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(nst + wave * BWP + c0), 16, voff, 0, 0, 0);
+    }
+  };
   auto stage = [&](int t, int n, int b) {
     if (DBG == 2) return;
     const NccMRec& e = rec[t];
@@ -140,7 +186,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 
   // the steps' level -> band column offsets, into LDS (before the pipeline)
   for (int i = tid; i < T * DC / 2; i += NW * 64) ((int*)colo_l)[i] = rec[i / (DC / 2)].colo[i % (DC / 2)];
-  stage(0, 0, 0);
+  // step t's scalars (cur) and step t+1's (nxt); horizontal lists only
+  StepInfo cur{}, nxt{};
+  if constexpr (!VERT) {
+    cur = load_info(0, 0);
+    if (T > 1) nxt = load_info(1, nn > 1 ? 1 : 0);
+    stage_h(cur, 0);
+  } else {
+    stage(0, 0, 0);
+  }
   const long zo = (long)a.z[ref] * Pv;
   // -Sr' and s_r of the tile's 64 x TH pixels (lane = column), as k_ncc_volume:
   // wave w takes rows w, w + 8, ... (one correctly rounded sqrt + divide per
@@ -151,7 +205,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
     for (int k = 0; k < 2 * R + 1; k++) {
       const uint2 v = pk[zo + pair_index(min(max(y - R + k, 0), H - 1), xc, W)];
-      const unsigned lo = v.x, hi = v.y & 0xffu;
+      const unsigned lo = v.x, hi = v.y & (K == 5 ? 0xffu : 0xffffffu);  // the window's K bytes
       s1 = dot4(lo, 0x01010101u, dot4(hi, 0x01010101u, s1));
       s2 = dot4(lo, lo, dot4(hi, hi, s2));
     }
@@ -160,52 +214,65 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     srl[lane * TH + o] = !valid ? __int_as_float(0x7fc00000) : (var != 0 ? 1.0f / sqrtf((float)var) : 0.0f);
     rsn_l[lane * TH + o] = -(float)s1;
   }
-  // the reference operands: pixel block (xb, yb) of this wave = columns
-  // x0 + 8 wave + 4 xb .. +3, rows y0 + 4 yb .. +3.  Lane l supplies row
-  // m = l & 15 (pixel xx = m >> 2, yy = m & 3) and row pair g = l >> 4 of the
-  // footprint: the 16-byte pk entry at column x0b, masked to the pixel's window
-  // (bytes xx .. xx+4 of a row; footprint rows yy .. yy+4)
-  i32x4 A[2][NYB];
+  // the reference operands.  K = 5: pixel block (xb, yb) of this wave =
+  // columns x0 + 8 wave + 4 xb .. +3, rows y0 + 4 yb .. +3; lane l supplies
+  // row m = l & 15 (pixel xx = m >> 2, yy = m & 3) and row pair g = l >> 4 of
+  // the footprint: the 16-byte pk entry at column x0b, masked to the pixel's
+  // window (bytes xx .. xx+4 of a row; footprint rows yy .. yy+4).  K = 7:
+  // block xb = columns x0 + 8 wave + 2 xb, +1, rows y0 .. y0 + 7; m = 8 xx + yy,
+  // the footprint rows y0 - 4 .. y0 + 11 (pairs g and g + 4: the block's two
+  // MFMAs), bytes xx .. xx+6, footprint rows yy + 1 .. yy + 7
+  i32x4 A[NBL][MF];
   {
-    const int mA = lane & 15, xxA = mA >> 2, yyA = mA & 3, g = lane >> 4;
-    unsigned msk[4];
+    const int mA = lane & 15, g = lane >> 4;
+    const int xxA = K == 5 ? mA >> 2 : mA >> 3, yyA = K == 5 ? mA & 3 : mA & 7;
+    unsigned msk[MF][4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int h = k >> 1, rr = 2 * g + h;
-      unsigned mk = 0;
+    for (int mf = 0; mf < MF; mf++)
 #pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const int t = 4 * (k & 1) + b;
-        if (t >= xxA && t <= xxA + 4 && rr >= yyA && rr <= yyA + 4) mk |= 0xffu << (8 * b);
+      for (int k = 0; k < 4; k++) {
+        const int h = k >> 1, rr = 2 * (g + 4 * mf) + h;
+        unsigned mk = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int t = 4 * (k & 1) + b;
+          const bool in = K == 5 ? (t >= xxA && t <= xxA + 4 && rr >= yyA && rr <= yyA + 4)
+                                 : (t >= xxA && t <= xxA + 6 && rr >= yyA + 1 && rr <= yyA + 7);
+          if (in) mk |= 0xffu << (8 * b);
+        }
+        msk[mf][k] = mk;
       }
-      msk[k] = mk;
-    }
 #pragma unroll
-    for (int xb = 0; xb < 2; xb++)
+    for (int xb = 0; xb < XB; xb++)
 #pragma unroll
-      for (int yb = 0; yb < NYB; yb++) {
-        const int xcol = min(x0 + 8 * wave + 4 * xb, W - 1);
-        const int pr = min(max((y0 >> 1) - 1 + 2 * yb + g, 0), Hp2 - 1);
-        const u32x4 v = *(const u32x4*)(pk + zo + (((long)pr * W + xcol) << 1));
-        A[xb][yb] = i32x4{(int)(v.x & msk[0]), (int)(v.y & msk[1]), (int)(v.z & msk[2]), (int)(v.w & msk[3])};
-      }
+      for (int yb = 0; yb < NYB; yb++)
+#pragma unroll
+        for (int mf = 0; mf < MF; mf++) {
+          const int xcol = min(x0 + 8 * wave + BXW * xb, W - 1);
+          const int pr = min(max(K == 5 ? (y0 >> 1) - 1 + 2 * yb + g : (y0 >> 1) - 2 + g + 4 * mf, 0), Hp2 - 1);
+          const u32x4 v = *(const u32x4*)(pk + zo + (((long)pr * W + xcol) << 1));
+          A[xb * NYB + yb][mf] = i32x4{(int)(v.x & msk[mf][0]), (int)(v.y & msk[mf][1]), (int)(v.z & msk[mf][2]),
+                                       (int)(v.w & msk[mf][3])};
+        }
   }
+  // this lane's output pixels of block (xb, yb): column 8 wave + pcol, rows
+  // prow .. prow + 3 of the tile (the MFMA's C[4 (l >> 4) + r][l & 15])
+  auto pcol = [&](int xb, int g) { return BXW * xb + (K == 5 ? g : g >> 1); };
+  auto prow = [&](int yb, int g) { return K == 5 ? 4 * yb : 4 * (g & 1); };
   __syncthreads();
 
-  float E[2][NYB][NDB][4];  // [xb][yb][level block][row]: max over the neighbours so far
-  float wv0[2][NYB][4], wv1[2][NYB][4];
-  unsigned wi0p[2][NYB][2];  // level of the smallest, rows (2p, 2p+1) as the halves of one register (0xffff: none)
+  float E[NBL][NDB][4];  // [block][level block][row]: max over the neighbours so far
+  float wv0[NBL][4], wv1[NBL][4];
+  unsigned wi0p[NBL][2];  // level of the smallest, rows (2p, 2p+1) as the halves of one register (0xffff: none)
 #pragma unroll
-  for (int xb = 0; xb < 2; xb++)
+  for (int k = 0; k < NBL; k++) {
 #pragma unroll
-    for (int yb = 0; yb < NYB; yb++) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        wv0[xb][yb][r] = kWtaInit;
-        wv1[xb][yb][r] = kWtaInit;
-      }
-      wi0p[xb][yb][0] = wi0p[xb][yb][1] = 0xffffffffu;
+    for (int r = 0; r < 4; r++) {
+      wv0[k][r] = kWtaInit;
+      wv1[k][r] = kWtaInit;
     }
+    wi0p[k][0] = wi0p[k][1] = 0xffffffffu;
+  }
   const i32x4 bias = i32x4{kMagicI, kMagicI, kMagicI, kMagicI};
 
   // fold chunk c's levels into the per-cell triples (k_ncc_volume's fold; this
@@ -220,10 +287,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
       for (int db = 0; db < NDB; db++) kill[db] = c * DC + 16 * db + (ln & 15) >= a.D ? INFINITY : 0.0f;
 #pragma unroll
-    for (int xb = 0; xb < 2; xb++)
+    for (int xb = 0; xb < XB; xb++)
 #pragma unroll
       for (int yb = 0; yb < NYB; yb++) {
-        const f32x4 sq = *(const f32x4*)(srl + (8 * wave + 4 * xb + (ln >> 4)) * TH + 4 * yb);
+        const int kb = xb * NYB + yb;
+        const f32x4 sq = *(const f32x4*)(srl + (8 * wave + pcol(xb, ln >> 4)) * TH + prow(yb, ln >> 4));
         // NDB = 2: this lane's two levels of the chunk, dl0 < dl1 = dl0 + 16,
         // folded as a pair: with lo / hi their smaller / larger cost, the
         // triple's new second smallest is min(max(v0, lo), v1, hi) (the second
@@ -237,7 +305,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
           f32x2 cst[NDB];
 #pragma unroll
           for (int db = 0; db < NDB; db++) {
-            const f32x2 e = f32x2{E[xb][yb][db][r], E[xb][yb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
+            const f32x2 e = f32x2{E[kb][db][r], E[kb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
             // NDB = 2: 1 - m without the clamp max(-1, m) -- a cost above 2 or
             // NaN (no valid neighbour window at the level) stands for the
             // clamped 2, restored at the merge; the pair fold below treats NaN
@@ -251,9 +319,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
           for (int h = 0; h < 2; h++) {
             const unsigned hm = h ? 0xffff0000u : 0x0000ffffu;
-            unsigned& wp = wi0p[xb][yb][r >> 1];
-            float& v0 = wv0[xb][yb][r + h];
-            float& v1 = wv1[xb][yb][r + h];
+            unsigned& wp = wi0p[kb][r >> 1];
+            float& v0 = wv0[kb][r + h];
+            float& v1 = wv1[kb][r + h];
             if constexpr (NDB == 2) {
               const float c0 = cst[0][h], c1 = cst[NDB - 1][h];  // NaN: absent (the clamped 2)
               const float lo = vmin3(c0, c1, INFINITY);  // the smaller present cost (+inf: none)
@@ -278,6 +346,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   auto step = [&](int t, int n, int cprev, auto first) {
     constexpr bool FIRST = decltype(first)::value;
     const int n1 = n + 1 == nn ? 0 : n + 1;
+    StepInfo pf{};  // step t+2's scalars, issued now, used two steps on
+    if constexpr (!VERT) {
+      const int n2 = n1 + 1 == nn ? 0 : n1 + 1;
+      if (t + 2 < T) pf = load_info(t + 2, n2);
+    }
     if (NB == 1 && t > 0) {  // this step's bands into the one buffer (step 0's: before the loop)
       stage(t, n, 0);
       __syncthreads();  // vmcnt(0): landed, for every wave
@@ -289,9 +362,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // 0's.  Where the band holds column -1 (tiles at the left image edge),
     // that entry becomes the pk plane's definition: column 0's bytes one place
     // later (its bytes 0..2 lie outside the image and meet masked taps only).
-    {
-      const int jf = rec[t].txmax - x0 - 1;  // band column of image column -1 (scalar)
-      if (jf >= 0 && jf + 1 < 64 + (rec[t].shp >> 16)) {  // inside the band's 64 + span columns
+    // (K = 7: a block's entry column is its 2-wide block's first column - tx,
+    // never left of a valid cell's neighbour column - 1 >= 2: nothing to fix)
+    if constexpr (K == 5) {
+      const int jf = (VERT ? rec[t].txmax : cur.tx) - x0 - 1;  // band column of image column -1 (scalar)
+      if (jf >= 0 && jf + 1 < 64 + ((VERT ? rec[t].shp : cur.shp) >> 16)) {  // inside the band's 64 + span columns
         if (tid < a.pk_pairs) {
           u32x4* e = nbuf_t + tid * BWP + jf;
           const u32x4 v = e[1];
@@ -300,7 +375,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         __syncthreads();
       }
     }
-    if (NB == 2 && t + 1 < T) stage(t + 1, n1, (t + 1) & 1);
+    if constexpr (!VERT) {
+      if (t + 1 < T) stage_h(nxt, (t + 1) & 1);
+    } else {
+      if (NB == 2 && t + 1 < T) stage(t + 1, n1, (t + 1) & 1);
+    }
     if (FIRST && cprev >= 0) fold(cprev);
     const u32x4* npk = nbuf_t;
     const u32x4* nst = npk + a.pk_pairs * BWP;
@@ -325,9 +404,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         iS1[db] = 4 * ((s1 >> 1) * BWP + col + g) + (s1 & 1);
       }
     }
-    auto bread = [&](int xb, int yb, int db) -> i32x4 {
-      if constexpr (!VERT) {
-        return __builtin_bit_cast(i32x4, npk[(2 * yb + g) * BWP + 8 * wave + 4 * xb + cl[db]]);
+    auto bread = [&](int xb, int yb, int db, int mf) -> i32x4 {
+      if constexpr (!VERT) {  // K = 5: pair 2 yb + g of the band; K = 7: pair g + 4 mf
+        const int pr = K == 5 ? 2 * yb + g : g + 4 * mf;
+        return __builtin_bit_cast(i32x4, npk[pr * BWP + 8 * wave + BXW * xb + cl[db]]);
       } else {
         const uint2* b2 = (const uint2*)npk;
         const int off = 2 * (2 * yb * BWP + 4 * xb);
@@ -335,12 +415,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         return i32x4{(int)lo.x, (int)lo.y, (int)hi.x, (int)hi.y};
       }
     };
-    auto finish = [&](int xb, int yb, int db, const i32x4& acc, const f32x4& nsr) {
-      f32x4 s0, s1;  // {a, a, b, b} of pixel rows 0, 1 and rows 2, 3 of the block
+    // {a, a, b, b} of pixel rows 0, 1 (s0) and rows 2, 3 (s1) of the block
+    auto sread = [&](int xb, int yb, int db, f32x4& s0, f32x4& s1) {
       if constexpr (!VERT) {
-        const int colS = 8 * wave + 4 * xb + cl[db] + g;  // stats band column of this lane's pixel column
-        s0 = __builtin_bit_cast(f32x4, nst[(2 * yb) * BWP + colS]);
-        s1 = __builtin_bit_cast(f32x4, nst[(2 * yb + 1) * BWP + colS]);
+        const int colS = 8 * wave + pcol(xb, g) + cl[db];  // stats band column of this lane's pixel column
+        const int sp = prow(yb, g) >> 1;                    // stats band pair of its first row
+        s0 = __builtin_bit_cast(f32x4, nst[sp * BWP + colS]);
+        s1 = __builtin_bit_cast(f32x4, nst[(sp + 1) * BWP + colS]);
       } else {
         const float* f = (const float*)nst;
         const int off = 4 * (2 * yb * BWP + 4 * xb);
@@ -348,33 +429,50 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         s0 = f32x4{f[q0], f[q1], f[q0 + 2], f[q1 + 2]};
         s1 = f32x4{f[q2], f[q3], f[q2 + 2], f[q3 + 2]};
       }
+    };
+    auto finish = [&](int xb, int yb, int db, const i32x4& acc, const f32x4& nsr, const f32x4& s0,
+                      const f32x4& s1) {
 #pragma unroll
       for (int p = 0; p < 2; p++) {
         const f32x4 sv = p ? s1 : s0;
         const f32x2 f = f32x2{__int_as_float(acc[2 * p]), __int_as_float(acc[2 * p + 1])} - f32x2{kMagicF, kMagicF};
         const f32x2 xv = __builtin_elementwise_fma(f32x2{nsr[2 * p], nsr[2 * p + 1]}, f32x2{sv.z, sv.w},
                                                    f * f32x2{sv.x, sv.y});
+        const int kb = xb * NYB + yb;
         if (FIRST) {
-          E[xb][yb][db][2 * p] = xv.x;
-          E[xb][yb][db][2 * p + 1] = xv.y;
+          E[kb][db][2 * p] = xv.x;
+          E[kb][db][2 * p + 1] = xv.y;
         } else {
-          E[xb][yb][db][2 * p] = vmax(E[xb][yb][db][2 * p], xv.x);
-          E[xb][yb][db][2 * p + 1] = vmax(E[xb][yb][db][2 * p + 1], xv.y);
+          E[kb][db][2 * p] = vmax(E[kb][db][2 * p], xv.x);
+          E[kb][db][2 * p + 1] = vmax(E[kb][db][2 * p + 1], xv.y);
         }
       }
     };
     // one level block at a time (at the 128-VGPR cap the paired form spilled 16-40 B)
 #pragma unroll
-    for (int k = 0; k < (DBG == 1 ? 0 : 2 * NYB); k++) {
+    for (int k = 0; k < (DBG == 1 ? 0 : NBL); k++) {
       const int xb = k / NYB, yb = k % NYB;
-      const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + 4 * xb + g) * TH + 4 * yb);
+      const f32x4 nsr = *(const f32x4*)(rsn_l + (8 * wave + pcol(xb, g)) * TH + prow(yb, g));
 #pragma unroll
       for (int db = 0; db < NDB; db++) {
-        const i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[xb][yb], bread(xb, yb, db), bias, 0, 0, 0);
-        finish(xb, yb, db, acc, nsr);
+        // the block's operand(s) and its neighbour stats issued together, ahead
+        // of the MFMA: one LDS latency per block on the wave's chain, not two
+        i32x4 bv[MF];
+#pragma unroll
+        for (int mf = 0; mf < MF; mf++) bv[mf] = bread(xb, yb, db, mf);
+        f32x4 s0, s1;
+        sread(xb, yb, db, s0, s1);
+        if (SPLIT) __builtin_amdgcn_sched_barrier(0);
+        i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[k][0], bv[0], bias, 0, 0, 0);
+        if constexpr (MF == 2) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[k][1], bv[1], acc, 0, 0, 0);
+        finish(xb, yb, db, acc, nsr, s0, s1);
       }
     }
     __syncthreads();  // NB = 2: step t+1's bands landed, this buffer free for t+2; NB = 1: free for t+1
+    if constexpr (!VERT) {
+      cur = nxt;
+      nxt = pf;
+    }
   };
   {
     int t = 0;
@@ -392,19 +490,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   float* m1 = m0 + 16 * kMfMergeStride;
   int* mi = (int*)(m1 + 16 * kMfMergeStride);
 #pragma unroll
-  for (int yb = 0; yb < NYB; yb++) {
+  for (int yb = 0; yb < TH / 4; yb++) {  // tile rows 4 yb .. 4 yb + 3
     {
-      const int ln = lane_now(), cls = ln & 15;
+      const int ln = lane_now(), cls = ln & 15, g = ln >> 4;
+      // K = 5: block row yb; K = 7: the lanes whose rows are these (g & 1 == yb)
+      const int kyb = K == 5 ? yb : 0;
+      if (K == 5 || (g & 1) == yb) {
 #pragma unroll
-      for (int xb = 0; xb < 2; xb++)
+        for (int xb = 0; xb < XB; xb++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int q = cls * kMfMergeStride + r * 64 + 8 * wave + 4 * xb + (ln >> 4);
-          const unsigned v = (r & 1) ? wi0p[xb][yb][r >> 1] >> 16 : wi0p[xb][yb][r >> 1] & 0xffffu;
-          m0[q] = wv0[xb][yb][r];
-          m1[q] = wv1[xb][yb][r];
-          mi[q] = v == 0xffffu ? -1 : (int)v;
-        }
+          for (int r = 0; r < 4; r++) {
+            const int kb = xb * NYB + kyb;
+            const int q = cls * kMfMergeStride + r * 64 + 8 * wave + pcol(xb, g);
+            const unsigned v = (r & 1) ? wi0p[kb][r >> 1] >> 16 : wi0p[kb][r >> 1] & 0xffffu;
+            m0[q] = wv0[kb][r];
+            m1[q] = wv1[kb][r];
+            mi[q] = v == 0xffffu ? -1 : (int)v;
+          }
+      }
     }
     __syncthreads();
     if (tid < 256) {
@@ -466,11 +569,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
-template <int BW, bool TAIL, bool VERT, int NDB, int NB, int DBG = 0>
+template <int K, int BW, bool TAIL, bool VERT, int NDB, int NB, int DBG = 0>
 int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec* plan, NccArgs& a,
                    const WtaOut& wo, int tmax) {
   constexpr int TH = 8, DC = 16 * NDB;
-  const int variant[8] = {5, TH, DC, 8, BW, VERT ? kParMixed : kParEven, 1, NB};
+  const int variant[8] = {K, TH, DC, 8, BW, VERT ? kParMixed : (K == 5 ? kParEven : kParOdd), 1, NB};
   std::copy(variant, variant + 8, ctx->ncc_last);
   a.tiles_x = (a.W + 63) / 64;
   a.ntiles = a.tiles_x * ((a.H + TH - 1) / TH);
@@ -478,7 +581,7 @@ int launch_mfma_bw(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccM
   a.nch = (a.D + DC - 1) / DC;
   const size_t lds = std::max((size_t)NB * 16 * (a.pk_pairs + a.st_pairs) * (BW + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
                      2 * 64 * TH * 4 + (size_t)tmax * DC * 2;
-  auto kern = k_ncc_mfma<BW, TAIL, VERT, NDB, NB, DBG>;
+  auto kern = k_ncc_mfma<K, BW, TAIL, VERT, NDB, NB, DBG>;
   MVS_HIP(raise_lds(ctx, (const void*)kern, lds), "hipFuncSetAttribute(ncc mfma lds)");
   const auto ev = kernel_events(ctx);  // (timing off: plain launch)
   hipExtLaunchKernelGGL(kern, dim3(8 * a.tiles_per_xcd), dim3(512), lds, ctx->stream, ev.first, ev.second, 0, stats, pk,
@@ -497,19 +600,21 @@ int launch_vert(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec
   if (!TAIL && NDB == 1 && NB == 2 && bwt == 80) {  // timing probe (C4's interior lists): MVS_NCC_MFMA_DBG=1 | 2
     const char* dbg = getenv("MVS_NCC_MFMA_DBG");
     const int dv = dbg ? atoi(dbg) : 0;
-    if (dv == 1) return launch_mfma_bw<80, false, true, 1, 2, 1>(ctx, stats, pk, pl, a, wo, tmax);
-    if (dv == 2) return launch_mfma_bw<80, false, true, 1, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
+    if (dv == 1) return launch_mfma_bw<5, 80, false, true, 1, 2, 1>(ctx, stats, pk, pl, a, wo, tmax);
+    if (dv == 2) return launch_mfma_bw<5, 80, false, true, 1, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
   }
-  if (TAIL || bwt == 128) return launch_mfma_bw<128, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);
-  return bwt == 80 ? launch_mfma_bw<80, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax)
-                   : launch_mfma_bw<96, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);
+  if (TAIL || bwt == 128) return launch_mfma_bw<5, 128, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);
+  return bwt == 80 ? launch_mfma_bw<5, 80, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax)
+                   : launch_mfma_bw<5, 96, TAIL, true, NDB, NB>(ctx, stats, pk, pl, a, wo, tmax);
 }
 
 }  // namespace
 
 // the matrix-core form's plan: one NccMRec per (chunk of 16 ndb levels, neighbour)
-NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl, int ndb) {
-  constexpr int TH = 8, R = 2, NR = TH + 2 * R, RW = sizeof(NccMRec) / 4;
+NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl, int ndb,
+                        int K) {
+  constexpr int TH = 8, RW = sizeof(NccMRec) / 4;
+  const int R = K / 2, NR = TH + 2 * R;
   const int DC = 16 * ndb;
   const int nch = (D + DC - 1) / DC;
   NccPlanM p;
@@ -531,7 +636,9 @@ NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, co
         tymax = std::max(tymax, ty_of(dl, n));
       }
       const int par = tymax & 1;  // the bands' first row (y0 - R - tymax, y0 - tymax) is o_j's parity off a pair
-      const int bhp = (par + NR + tymax - tymin + 1) >> 1, shp = (par + TH + tymax - tymin + 1) >> 1;
+      // (K = 7, horizontal only: the 8 pairs of rows y0 - 4 .. y0 + TH + 3)
+      const int bhp = K == 7 ? (TH + 8) / 2 : (par + NR + tymax - tymin + 1) >> 1;
+      const int shp = (par + TH + tymax - tymin + 1) >> 1;
       int32_t* e = p.table.data() + ((size_t)c * nn + n) * RW;
       e[0] = txmax;
       e[1] = tymax;
@@ -560,9 +667,14 @@ size_t mfma_lds_bytes(const NccPlanM& p, int band_w, int nb, int tmax, int D) {
 }
 
 int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
-                    const WtaOut& wo, int bw, int tmax, bool vert, int ndb, int nb) {
+                    const WtaOut& wo, int bw, int tmax, bool vert, int ndb, int nb, int K) {
   const NccMRec* pl = (const NccMRec*)plan_dev;
   const bool tail = a.D % (16 * ndb) != 0;
+  if (K == 7) {  // horizontal lists, 16-level chunks, double-buffered
+    if (tail) return launch_mfma_bw<7, 192, true, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax);
+    return bw <= 128 ? launch_mfma_bw<7, 128, false, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax)
+                     : launch_mfma_bw<7, 192, false, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax);
+  }
   if (vert) {
     if (ndb == 2 && nb == 2)
       return tail ? launch_vert<true, 2, 2>(ctx, stats, pk, pl, a, wo, bw, tmax)
@@ -576,9 +688,9 @@ int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int
     return tail ? launch_vert<true, 1, 1>(ctx, stats, pk, pl, a, wo, bw, tmax)
                 : launch_vert<false, 1, 1>(ctx, stats, pk, pl, a, wo, bw, tmax);
   }
-  if (tail) return launch_mfma_bw<192, true, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
-  return bw <= 128 ? launch_mfma_bw<128, false, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax)
-                   : launch_mfma_bw<192, false, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
+  if (tail) return launch_mfma_bw<5, 192, true, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
+  return bw <= 128 ? launch_mfma_bw<5, 128, false, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax)
+                   : launch_mfma_bw<5, 192, false, false, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
 }
 
 }  // namespace ncc

@@ -379,15 +379,16 @@ def test_box_planes(engine, K, W, H):
     assert np.array_equal(got_pk, pk), f"packed rows K{K} {W}x{H}"
 
 
-@pytest.mark.parametrize("D,nn", [(1600, 16), (3200, 16)])
+@pytest.mark.parametrize("D,nn", [(1600, 16), (4000, 16)])
 def test_fused_large_d_horizontal(eng, D, nn):
     """A horizontal list whose matrix-core run would not fit the LDS (ADVICE
     r05): 16 horizontal neighbours (a 17x1 array, 8 views either side) and
     fractional levels 0.05 apart, so every 32-level chunk's band stays within
     the 192-column pitch.  k_ncc_mfma keeps a run's level offsets in LDS
     (chunks x neighbours x 64 B): at D = 1600 they fit and the matrix-core
-    form runs (DPW >= 16 in the report); at D = 3200 they would pass 160 KB and
-    the scalar fused kernel takes the view.  Both bit-exact against the oracle."""
+    form runs (DPW >= 16 in the report); at D = 4000 (128 KB of offsets beside
+    the 128-column bands) they would pass 160 KB and the scalar fused kernel
+    takes the view.  Both bit-exact against the oracle."""
     aw, W, H, z = 17, 72, 12, 8
     levels = (np.arange(D, dtype=np.float32) * np.float32(0.05)).astype(np.float32)
     vs, sn = params.flatten_subsets(params.neighbour_lists(aw, 1, nn // 2, 0))
@@ -403,3 +404,34 @@ def test_fused_large_d_horizontal(eng, D, nn):
     assert v["FUSE"] == 1 and (v["DPW"] >= 16) == (D == 1600), v  # DPW >= 16: the matrix-core form
     same(fd, od, f"fused disp D{D}")
     same(fc, oc, f"fused conf D{D}")
+
+
+@pytest.mark.parametrize("W,H,dmax,aw,nh", [(150, 27, 63, 5, 4), (130, 40, 100, 5, 4), (64, 8, 15, 3, 1),
+                                            (200, 33, 40, 7, 3), (97, 19, 31, 4, 2)])
+def test_mfma_k7(eng, monkeypatch, W, H, dmax, aw, nh):
+    """The matrix-core K = 7 fused sweep (k_ncc_mfma<7, ...>: 2 x 8-pixel
+    blocks, two MFMAs per level block over the 16-row footprint, 16-level
+    chunks) on horizontal lists: ragged tiles (W, H off the 64 x 8 tile, odd H),
+    image borders, whole and partial last chunks (D = 16, 64 / D = 101, 41, 32),
+    shifts up to 4 columns per level (band pitch 128, 192 with a tail).  Every
+    reference view against the oracle and against the scalar fused kernel
+    (MVS_NCC_MFMA7=0), bit for bit."""
+    stack, _ = synth.make_stack(W, H, aw, 1, 0, dmax, 1.0, 0x7A + W + H)
+    cam = _array(aw, 1, 0, dmax, nh=nh)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    box = eng.box_stats(l8, 7)
+    l8h = l8.cpu().numpy()
+    for z in range(aw):
+        want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, 1.0, 7, z)
+        od, oc = orc.wta(want, cam.levels)
+        monkeypatch.delenv("MVS_NCC_MFMA7", raising=False)
+        fd, fc = eng.ncc_wta(l8, box, cam, z, 7)
+        v = eng.ncc_last_variant()
+        assert (v["K"], v["DPW"], v["FUSE"]) == (7, 16, 1), v  # DPW 16: the matrix-core form, 16-level chunks
+        same(fd, od, f"k7 mfma disp z{z}")
+        same(fc, oc, f"k7 mfma conf z{z}")
+        monkeypatch.setenv("MVS_NCC_MFMA7", "0")
+        sd, sc = eng.ncc_wta(l8, box, cam, z, 7)
+        assert eng.ncc_last_variant()["DPW"] < 16
+        same(sd, fd, f"k7 scalar vs mfma disp z{z}")
+        same(sc, fc, f"k7 scalar vs mfma conf z{z}")

@@ -786,8 +786,10 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   const char* mfe = getenv("MVS_NCC_MFMA");
   const char* mfv = getenv("MVS_NCC_MFMA_V");
   const char* mf7 = getenv("MVS_NCC_MFMA7");
+  // (its band DMA addresses one view's plane by 32-bit byte offsets)
   const bool mf_on = !vol && (K == 5 || (K == 7 && !(mf7 && atoi(mf7) == 0))) && !(mfe && atoi(mfe) == 0) &&
-                     !ctx->ncc_nw && !ctx->ncc_dpw && !ctx->ncc_general && !ctx->ncc_bw;
+                     !ctx->ncc_nw && !ctx->ncc_dpw && !ctx->ncc_general && !ctx->ncc_bw &&
+                     (long)W * (H + (H & 1)) * 8 < 0x7fffffffL;
   const int mfv_form = mfv ? atoi(mfv) : 0;  // 0: off, 1: automatic, else the form
   std::vector<char> mf(n, 0);
   std::vector<NccPlanM> mplan(n);
@@ -872,7 +874,18 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
         a.nn[j - i] = sn_host[z];
         a.plan[j - i] = (int)(table.size() / 32);  // 128-B NccMRec records
         for (int k = 0; k < sn_host[z]; k++) a.view[j - i][k] = views[j][k];
+        // each record's neighbour plane as a byte offset (words 22, 23): the
+        // kernel rebases its band DMA on it with no per-step multiply
+        const size_t r0 = table.size();
         table.insert(table.end(), mplan[j].table.begin(), mplan[j].table.end());
+        for (size_t rr = r0; rr < table.size(); rr += 32) {
+          const int nloc = (int)((rr - r0) / 32) % sn_host[z];
+          const unsigned long long off = (unsigned long long)views[j][nloc] * (unsigned long long)W *
+                                         (unsigned long long)((H + 1) >> 1) * 16ull;  // Pv uint2 = 16 B per (pair row, column)
+          table[rr + 22] = (int32_t)(off & 0xffffffffull);
+          table[rr + 23] = (int32_t)(off >> 32);
+          a.txmax_all = std::max(a.txmax_all, table[rr]);
+        }
         j++;
       }
       a.nref = j - i;

@@ -23,6 +23,8 @@ struct NccArgs {
   int W, H, D, nref;
   int tiles_x, ntiles, tiles_per_xcd, nch;  // XCD-aware work map over nref x ntiles tiles (see k_ncc_volume)
   int pk_pairs, st_pairs;  // LDS band heights in row pairs; the pair-row stride is the template BW
+  int txmax_all;           // (matrix-core runs) the largest band origin shift of any step: tiles with
+                           // x0 >= it never hold image column -1 in a band
   // per reference view r of the launch: view id, neighbour count, first plan
   // record, neighbour view ids
   int z[kMaxRef], nn[kMaxRef], plan[kMaxRef];
@@ -158,6 +160,44 @@ __device__ __forceinline__ void read_stat_pairs(const u32x4* col, int r0, f32x4 
 // keeps every partial sum without the accumulator copies the VOP2 v_dot4c
 // form forces.  The Makefile builds this file with the dot6 feature (v_dot4c)
 // off, so the compiler selects the VOP3P form and still tracks its hazards.
+// s_waitcnt vmcnt(min(n, 6)) (n >= 0; a count above 6 waits for 6: still
+// correct for a caller that needs at most n outstanding, only earlier)
+__device__ __forceinline__ void wait_vm_le(int n) {
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    case 1: __builtin_amdgcn_s_waitcnt(0x0f71); break;
+    case 2: __builtin_amdgcn_s_waitcnt(0x0f72); break;
+    case 3: __builtin_amdgcn_s_waitcnt(0x0f73); break;
+    case 4: __builtin_amdgcn_s_waitcnt(0x0f74); break;
+    case 5: __builtin_amdgcn_s_waitcnt(0x0f75); break;
+    default: __builtin_amdgcn_s_waitcnt(0x0f76); break;
+  }
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 6] (n > 6: vmcnt(6)), then
+// s_barrier -- the selection inside one asm block, so the compiler sees no
+// branch (a C-level switch split the step and spilled the fold's registers)
+__device__ __forceinline__ void wait_vm_barrier(int n) {
+  asm volatile(
+      "s_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 10f\n\t"
+      "s_cmp_eq_u32 %0, 1\n\ts_cbranch_scc1 11f\n\t"
+      "s_cmp_eq_u32 %0, 2\n\ts_cbranch_scc1 12f\n\t"
+      "s_cmp_eq_u32 %0, 3\n\ts_cbranch_scc1 13f\n\t"
+      "s_cmp_eq_u32 %0, 4\n\ts_cbranch_scc1 14f\n\t"
+      "s_cmp_eq_u32 %0, 5\n\ts_cbranch_scc1 15f\n\t"
+      "s_waitcnt vmcnt(6)\n\ts_branch 19f\n"
+      "10:\n\ts_waitcnt vmcnt(0)\n\ts_branch 19f\n"
+      "11:\n\ts_waitcnt vmcnt(1)\n\ts_branch 19f\n"
+      "12:\n\ts_waitcnt vmcnt(2)\n\ts_branch 19f\n"
+      "13:\n\ts_waitcnt vmcnt(3)\n\ts_branch 19f\n"
+      "14:\n\ts_waitcnt vmcnt(4)\n\ts_branch 19f\n"
+      "15:\n\ts_waitcnt vmcnt(5)\n"
+      "19:\n\ts_barrier"
+      :
+      : "s"(n)
+      : "memory", "scc");
+}
+
 // the lane id, recomputed where it is used (volatile: never hoisted, so it is
 // never a long-lived value the register allocator would spill)
 __device__ __forceinline__ int lane_now() {

@@ -59,7 +59,9 @@ struct alignas(128) NccMRec {
   int bhp, shp;      // pk / stats pair rows to stage | (column span) << 16, as NccRec
   int colo[16];      // 32 x int16: per level j of the chunk, txmax - tx(j) (band column of reference column x0)
                      // | o_j << 8 (VERT: band row of the level's footprint)
-  int pad[12];
+  int pad0[2];
+  unsigned off_lo, off_hi;  // the neighbour's plane: byte offset from the stack's first (set by the launcher)
+  int pad[8];
 };
 static_assert(sizeof(NccMRec) == 128, "one 128-B record per (chunk, neighbour)");
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   static_assert(NDB == 1 || NDB == 2, "one or two 16-level blocks per chunk");
   static_assert(K == 5 || K == 7, "5 x 5 or 7 x 7 windows");
   static_assert(K == 5 || !VERT, "K = 7: horizontal lists only");
-  static_assert(VERT || NB == 2, "the horizontal form is double-buffered");
+  static_assert(VERT || NB == 2 || NB == 3, "the horizontal form is double- or triple-buffered");
   static_assert(VERT || NDB == (K == 5 ? 2 : 1), "horizontal chunks: 32 levels (K = 5), 16 (K = 7: A takes 32 VGPRs)");
   constexpr int R = K / 2, NW = 8, TH = 8, DC = 16 * NDB, NK = K * K;
   // pixel blocks per wave: XB across (BXW columns each) x NYB down; MF MFMAs per block and level block
@@ -131,28 +133,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   // (base = the neighbour's plane row, 32-bit lane offsets: the clamped
   // column x 16 B), no per-lane 64-bit address arithmetic.
   struct StepInfo {
-    int tx, shp, view;  // raw record words: nothing computed on them until they are used
+    int tx, shp;      // raw record words: nothing computed on them until they are used
+    unsigned lo, hi;  // the neighbour plane's byte offset
   };
   auto load_info = [&](int t, int n) -> StepInfo {
     const NccMRec& e = rec[t];
-    return StepInfo{e.txmax, e.shp, a.view[ref][n]};
+    return StepInfo{e.txmax, e.shp, e.off_lo, e.off_hi};
   };
   const int lane_x = x0 + lane;
   auto stage_h = [&](const StepInfo& e, int b) {
     if (DBG == 2) return;
     const int span = e.shp >> 16, nblk = (span + 127) >> 6;
-    const long vo = (long)e.view * Pv;
+    const unsigned long long vo = (unsigned long long)e.hi << 32 | e.lo;
     u32x4* npk = nbase + b * nbuf;
     u32x4* nst = npk + a.pk_pairs * BWP;
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(pk + vo + pk_row), 0, 16 * W, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(stats + vo + st_row), 0, 16 * W, 0x00020000);
-    for (int cb = 0; cb < nblk; cb++) {
-      const int c0 = min(cb * 64, span);
-      const int voff = 16 * min(max(lane_x - e.tx + c0, 0), W - 1);
-      if (wave < bhp)
+    // the wave's roles (pk row w < bhp, stats row w < shp) decided once per step, not per piece
+    if (wave < shp) {
+      const __amdgpu_buffer_rsrc_t rp =
+          __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)pk + vo + 8 * pk_row), 0, 16 * W, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)stats + vo + 8 * st_row), 0, 16 * W, 0x00020000);
+      for (int cb = 0; cb < nblk; cb++) {
+        const int c0 = min(cb * 64, span);
+        const int voff = 16 * min(max(lane_x - e.tx + c0, 0), W - 1);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (lds_ptr_t)(npk + wave * BWP + c0), 16, voff, 0, 0, 0);
-      if (wave < shp)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(nst + wave * BWP + c0), 16, voff, 0, 0, 0);
+      }
+    } else if (wave < bhp) {
+      const __amdgpu_buffer_rsrc_t rp =
+          __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)pk + vo + 8 * pk_row), 0, 16 * W, 0x00020000);
+      for (int cb = 0; cb < nblk; cb++) {
+        const int c0 = min(cb * 64, span);
+        const int voff = 16 * min(max(lane_x - e.tx + c0, 0), W - 1);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (lds_ptr_t)(npk + wave * BWP + c0), 16, voff, 0, 0, 0);
+      }
     }
   };
   auto stage = [&](int t, int n, int b) {
@@ -187,11 +201,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   // the steps' level -> band column offsets, into LDS (before the pipeline)
   for (int i = tid; i < T * DC / 2; i += NW * 64) ((int*)colo_l)[i] = rec[i / (DC / 2)].colo[i % (DC / 2)];
   // step t's scalars (cur) and step t+1's (nxt); horizontal lists only
-  StepInfo cur{}, nxt{};
+  // NB = 3 (horizontal): nx2 = step t+2's, staged at step t, two steps ahead
+  auto nmod = [&](int v) { return v >= nn ? v - nn : v; };  // (v < 2 nn)
+  StepInfo cur{}, nxt{}, nx2{};
   if constexpr (!VERT) {
     cur = load_info(0, 0);
-    if (T > 1) nxt = load_info(1, nn > 1 ? 1 : 0);
+    if (T > 1) nxt = load_info(1, nmod(1 % nn));
+    if (NB == 3 && T > 2) nx2 = load_info(2, nmod(2 % nn));
     stage_h(cur, 0);
+    if (NB == 3 && T > 1) stage_h(nxt, 1);
   } else {
     stage(0, 0, 0);
   }
@@ -341,21 +359,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
   };
 
+  int bt = 0;  // NB = 3: the buffer of step t (t % 3)
   // one pipeline step t = c * nn + n (chunks outer, neighbours inner; the
   // chunk's first neighbour assigns E, as k_ncc_volume's PEEL)
   auto step = [&](int t, int n, int cprev, auto first) {
     constexpr bool FIRST = decltype(first)::value;
     const int n1 = n + 1 == nn ? 0 : n + 1;
-    StepInfo pf{};  // step t+2's scalars, issued now, used two steps on
+    StepInfo pf{};  // step t+NB's scalars, issued now, used NB - 1 steps on
     if constexpr (!VERT) {
       const int n2 = n1 + 1 == nn ? 0 : n1 + 1;
-      if (t + 2 < T) pf = load_info(t + 2, n2);
+      if (t + NB < T) pf = load_info(t + NB, NB == 2 ? n2 : nmod(n2 + 1));
     }
     if (NB == 1 && t > 0) {  // this step's bands into the one buffer (step 0's: before the loop)
       stage(t, n, 0);
       __syncthreads();  // vmcnt(0): landed, for every wave
     }
-    u32x4* const nbuf_t = nbase + (NB == 2 ? (t & 1) * nbuf : 0);
+    u32x4* const nbuf_t = nbase + (NB == 2 ? (t & 1) : NB == 3 ? bt : 0) * nbuf;
     // A block's B entry sits at column x0b - tx, up to 3 columns left of its
     // cells' neighbour pixels: a valid cell (neighbour column 2, xx = 3) reads
     // the entry of image column -1, which the clamped DMA filled with column
@@ -364,7 +383,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // later (its bytes 0..2 lie outside the image and meet masked taps only).
     // (K = 7: a block's entry column is its 2-wide block's first column - tx,
     // never left of a valid cell's neighbour column - 1 >= 2: nothing to fix)
-    if constexpr (K == 5) {
+    if (K == 5 && (VERT || x0 < a.txmax_all)) {  // (tiles right of every shift: never)
       const int jf = (VERT ? rec[t].txmax : cur.tx) - x0 - 1;  // band column of image column -1 (scalar)
       if (jf >= 0 && jf + 1 < 64 + ((VERT ? rec[t].shp : cur.shp) >> 16)) {  // inside the band's 64 + span columns
         if (tid < a.pk_pairs) {
@@ -375,8 +394,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         __syncthreads();
       }
     }
-    if constexpr (!VERT) {
+    int pieces = 0;  // NB = 3: this wave's LDS-DMA pieces of step t+2 (the barrier's count)
+    if constexpr (!VERT && NB == 2) {
       if (t + 1 < T) stage_h(nxt, (t + 1) & 1);
+    } else if constexpr (!VERT) {
+      if (t + 2 < T) {
+        stage_h(nx2, bt == 0 ? 2 : bt - 1);  // (t + 2) % 3
+        const int nb2 = ((nx2.shp >> 16) + 127) >> 6;
+        pieces = (wave < bhp ? nb2 : 0) + (wave < shp ? nb2 : 0);
+      }
     } else {
       if (NB == 2 && t + 1 < T) stage(t + 1, n1, (t + 1) & 1);
     }
@@ -468,10 +494,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         finish(xb, yb, db, acc, nsr, s0, s1);
       }
     }
-    __syncthreads();  // NB = 2: step t+1's bands landed, this buffer free for t+2; NB = 1: free for t+1
+    if constexpr (!VERT && NB == 3) {
+      // step t+1's bands landed (this wave's pieces of it are older than its
+      // `pieces` of step t+2: loads retire in order), then the barrier: every
+      // wave's; buffer t % 3 is free for step t+3 (staged at step t+1)
+      wait_vm_barrier(pieces);  // (a memory clobber: no LDS access moves across it; no vmcnt(0) added)
+    } else {
+      __syncthreads();  // NB = 2: step t+1's bands landed, this buffer free for t+2; NB = 1: free for t+1
+    }
     if constexpr (!VERT) {
       cur = nxt;
-      nxt = pf;
+      if constexpr (NB == 3) {
+        nxt = nx2;
+        nx2 = pf;
+        bt = bt == 2 ? 0 : bt + 1;
+      } else {
+        nxt = pf;
+      }
     }
   };
   {
@@ -666,14 +705,38 @@ size_t mfma_lds_bytes(const NccPlanM& p, int band_w, int nb, int tmax, int D) {
          2 * 64 * 8 * 4 + (size_t)tmax * 16 * p.ndb * 2;
 }
 
+// the LDS bytes of a launch with these band heights, pitch bw (+1), nb buffers, dc levels per chunk
+static size_t mfma_lds_bytes_nb(const NccArgs& a, int bw, int nb, int tmax, int dc) {
+  return std::max((size_t)nb * 16 * (a.pk_pairs + a.st_pairs) * (bw + 1), (size_t)3 * 16 * kMfMergeStride * 4) +
+         2 * 64 * 8 * 4 + (size_t)tmax * dc * 2;
+}
+
 int launch_ncc_mfma(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const int32_t* plan_dev, NccArgs& a,
                     const WtaOut& wo, int bw, int tmax, bool vert, int ndb, int nb, int K) {
   const NccMRec* pl = (const NccMRec*)plan_dev;
   const bool tail = a.D % (16 * ndb) != 0;
-  if (K == 7) {  // horizontal lists, 16-level chunks, double-buffered
+  // timing probe (MVS_NCC_MFMA_DBG=1: no MFMA / finish, 2: no band DMA), C2's and C5's forms
+  const char* dbg = getenv("MVS_NCC_MFMA_DBG");
+  const int dv = dbg ? atoi(dbg) : 0;
+  if (dv && !vert && !tail) {
+    if (K == 7 && bw <= 128)
+      return dv == 1 ? launch_mfma_bw<7, 128, false, false, 1, 2, 1>(ctx, stats, pk, pl, a, wo, tmax)
+                     : launch_mfma_bw<7, 128, false, false, 1, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
+    if (K == 5 && bw > 128)
+      return dv == 1 ? launch_mfma_bw<5, 192, false, false, 2, 2, 1>(ctx, stats, pk, pl, a, wo, tmax)
+                     : launch_mfma_bw<5, 192, false, false, 2, 2, 2>(ctx, stats, pk, pl, a, wo, tmax);
+  }
+  if (K == 7) {  // horizontal lists, 16-level chunks
+    // the 128-column pitch triple-buffered (bands two steps ahead; 2 x 3
+    // buffers of 24.8 KB keep two workgroups per CU), else double-buffered;
+    // MVS_NCC_MFMA7_NB=3 (read per call): the triple-buffered form (measured slower, opt-in)
+    const char* nbe = getenv("MVS_NCC_MFMA7_NB");
+    const bool nb3 = nbe && atoi(nbe) == 3 && mfma_lds_bytes_nb(a, 128, 3, tmax, 16) <= (size_t)80 * 1024;
     if (tail) return launch_mfma_bw<7, 192, true, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax);
-    return bw <= 128 ? launch_mfma_bw<7, 128, false, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax)
-                     : launch_mfma_bw<7, 192, false, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax);
+    if (bw <= 128)
+      return nb3 ? launch_mfma_bw<7, 128, false, false, 1, 3>(ctx, stats, pk, pl, a, wo, tmax)
+                 : launch_mfma_bw<7, 128, false, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax);
+    return launch_mfma_bw<7, 192, false, false, 1, 2>(ctx, stats, pk, pl, a, wo, tmax);
   }
   if (vert) {
     if (ndb == 2 && nb == 2)

@@ -413,9 +413,10 @@ def test_mfma_k7(eng, monkeypatch, W, H, dmax, aw, nh):
     blocks, two MFMAs per level block over the 16-row footprint, 16-level
     chunks) on horizontal lists: ragged tiles (W, H off the 64 x 8 tile, odd H),
     image borders, whole and partial last chunks (D = 16, 64 / D = 101, 41, 32),
-    shifts up to 4 columns per level (band pitch 128, 192 with a tail).  Every
-    reference view against the oracle and against the scalar fused kernel
-    (MVS_NCC_MFMA7=0), bit for bit."""
+    shifts up to 4 columns per level (band pitch 128, 192 with a tail), the
+    triple-buffered form and the double-buffered one (MVS_NCC_MFMA7_NB=2).
+    Every reference view against the oracle and against the scalar fused
+    kernel (MVS_NCC_MFMA7=0), bit for bit."""
     stack, _ = synth.make_stack(W, H, aw, 1, 0, dmax, 1.0, 0x7A + W + H)
     cam = _array(aw, 1, 0, dmax, nh=nh)
     lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
@@ -430,6 +431,18 @@ def test_mfma_k7(eng, monkeypatch, W, H, dmax, aw, nh):
         assert (v["K"], v["DPW"], v["FUSE"]) == (7, 16, 1), v  # DPW 16: the matrix-core form, 16-level chunks
         same(fd, od, f"k7 mfma disp z{z}")
         same(fc, oc, f"k7 mfma conf z{z}")
+        # the 128-column pitch without a partial chunk also has a triple-
+        # buffered form (bands two steps ahead, counted vmcnt before each
+        # barrier; MVS_NCC_MFMA7_NB picks it): the other form, the same bits
+        tail = (dmax + 1) % 16 != 0
+        if not tail and v["BW"] == 128:
+            other = 2 if v["NB"] == 3 else 3
+            monkeypatch.setenv("MVS_NCC_MFMA7_NB", str(other))
+            d2, c2 = eng.ncc_wta(l8, box, cam, z, 7)
+            assert eng.ncc_last_variant()["NB"] == other
+            same(d2, fd, f"k7 mfma double- vs triple-buffered disp z{z}")
+            same(c2, fc, f"k7 mfma double- vs triple-buffered conf z{z}")
+            monkeypatch.delenv("MVS_NCC_MFMA7_NB")
         monkeypatch.setenv("MVS_NCC_MFMA7", "0")
         sd, sc = eng.ncc_wta(l8, box, cam, z, 7)
         assert eng.ncc_last_variant()["DPW"] < 16

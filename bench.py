@@ -523,9 +523,10 @@ def bench(args, world, rank, local):
             res["roofline_sweep"]["kernel_timing"] = ("start / stop events of each fused launch's own dispatch "
                                                       "(hipExtLaunchKernel), warmup + timed steps")
         if per_view is not None and not per_view.get("stale"):
+            valu_only = per_view["insts"] - per_view.get("mfma", 0.0)  # (SQ_INSTS_VALU counts the MFMAs)
             res["roofline_sweep"].update({
-                "valu_wave_insts_per_view": round(per_view["insts"]),
-                "valu_issue_frac": round(per_view["insts"] * vpc / t_f / VALU_PEAK, 4),
+                "valu_wave_insts_per_view": round(valu_only),
+                "valu_issue_frac": round(valu_only * vpc / t_f / VALU_PEAK, 4),
                 "valu_peak": VALU_PEAK_NOTE,
                 "valu_source": per_view["source"]})
         if per_view is not None:

@@ -1,0 +1,16 @@
+# round-6 final records: the GPU suite, smoke, the driver's bench command, every
+# other configuration's line, and a kernel trace of the driver's command with
+# the headline kernel's trace-vs-line check.  Summaries under gpurun_out/r06i;
+# the rocprof database is removed (gpurun returns at most 64 MiB).
+set -u
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r06i; mkdir -p $O
+bash scripts/gpu_pass.sh r06i tests smoke bench bench:c1 bench:c3 bench:c4 bench:c5 bench:ref || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace_drv -o run -- python3 bench.py --gpus 1 --steps 20 \
+  --warmup 5 > $O/trace_driver_bench.json 2> $O/trace_drv.err || { tail -5 $O/trace_drv.err; exit 1; }
+python3 scripts/kstats.py $O/trace_drv > $O/c2_driver_kernel_trace.txt 2>&1
+python3 scripts/headline_kernel_check.py $O/trace_drv $O/trace_driver_bench.json 20 5 > $O/headline_check.json 2>&1
+cat $O/headline_check.json
+rm -rf $O/trace_drv
+du -sh gpurun_out

@@ -36,7 +36,7 @@ def main():
     import bench
     pv = bench._valu_insts_fused_per_view(line["config"].get("name", "c2"), line["config"]["width"],
                                           line["config"]["height"], line["config"]["hypotheses"])
-    issue = pv["insts"] + 2.0 * pv.get("mfma", 0.0)
+    issue = pv["insts"] - pv.get("mfma", 0.0)  # vector-ALU instructions only, as bench.py (SQ_INSTS_VALU counts MFMAs)
     frac = issue * views / (avg_ms * 1e-3) / bench.VALU_PEAK
     out = {"trace_dispatches_fused": len(fused), "headline_pass_launches": len(head),
            "trace_avg_ms_per_launch_timed": round(avg_ms, 4), "trace_avg_ms_per_view": round(avg_ms / views, 4),

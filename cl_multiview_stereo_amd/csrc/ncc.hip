@@ -212,6 +212,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
   // one moved back to end at column 64 + span: it never writes past the row,
   // so the row pitch BW need only hold 64 + the widest span (not a multiple
   // of 64), and the overlapped columns get the same bytes twice.
+  // A view plane under 2 GB (plane32) is staged through buffer descriptors:
+  // the lane's 32-bit offset (clamped column x 16 B) fixed per piece, the
+  // clamped pair row as the scalar offset -- no per-lane 64-bit address per row
+  // (C4's tall bands stage up to ~40 pair rows per step)
   auto stage = [&](int t, int n, int b) {
     const NccRec& e = rec[NW * t];
     const int bhp = e.bhp, shp = e.shp & 0xffff, span = e.shp >> 16, nblk = (span + 127) >> 6;
@@ -219,6 +223,22 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     const long vo = (long)a.view[ref][n] * Pv;
     u32x4* npk = nbase + b * nbuf;
     u32x4* nst = npk + a.pk_pairs * BW;
+    if (a.plane32) {
+      const int pb = 16 * W;  // bytes per pair row
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(pk + vo), 0, pb * Hp2, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(stats + vo), 0, pb * Hp2, 0x00020000);
+      for (int cb = 0; cb < nblk; cb++) {
+        const int c0 = min(cb * 64, span);
+        const int voff = 16 * min(max(x0 - e.txmax + c0 + lane, 0), W - 1);
+        for (int i = wave; i < bhp; i += NW)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (lds_ptr_t)(npk + i * BW + c0), 16, voff,
+                                                   pb * min(max(pm0 + i, 0), Hp2 - 1), 0, 0);
+        for (int i = wave; i < shp; i += NW)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(nst + i * BW + c0), 16, voff,
+                                                   pb * min(max(sm0 + i, 0), Hp2 - 1), 0, 0);
+      }
+      return;
+    }
     for (int cb = 0; cb < nblk; cb++) {
       const int c0 = min(cb * 64, span);
       const int xx = min(max(x0 - e.txmax + c0 + lane, 0), W - 1);
@@ -925,6 +945,9 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
     a.W = W;
     a.H = H;
     a.D = D;
+    // (band DMA by 32-bit buffer offsets; MVS_NCC_PLANE32=0, read per call: the 64-bit addresses, A/B)
+    const char* p32 = getenv("MVS_NCC_PLANE32");
+    a.plane32 = (long)W * (H + (H & 1)) * 8 < 0x7fffffffL && !(p32 && atoi(p32) == 0);
     a.nref = j - i;
     a.pk_pairs = pkp;
     a.st_pairs = stp;

@@ -25,6 +25,7 @@ struct NccArgs {
   int pk_pairs, st_pairs;  // LDS band heights in row pairs; the pair-row stride is the template BW
   int txmax_all;           // (matrix-core runs) the largest band origin shift of any step: tiles with
                            // x0 >= it never hold image column -1 in a band
+  int plane32;             // (scalar kernels) a view plane is under 2 GB: band DMA by buffer descriptors
   // per reference view r of the launch: view id, neighbour count, first plan
   // record, neighbour view ids
   int z[kMaxRef], nn[kMaxRef], plan[kMaxRef];

@@ -448,3 +448,37 @@ def test_mfma_k7(eng, monkeypatch, W, H, dmax, aw, nh):
         assert eng.ncc_last_variant()["DPW"] < 16
         same(sd, fd, f"k7 scalar vs mfma disp z{z}")
         same(sc, fc, f"k7 scalar vs mfma conf z{z}")
+
+
+@pytest.mark.parametrize("geom", ["c4_knn5", "horizontal_forced"])
+def test_scalar_band_dma_forms(eng, monkeypatch, geom):
+    """The scalar kernels' band staging: buffer descriptors with the pair row
+    as the scalar offset (the default for view planes under 2 GB) against the
+    64-bit per-lane addresses (MVS_NCC_PLANE32=0), both against the oracle:
+    C4's 5-NN lists (tall single-buffered vertical / diagonal bands, the
+    corner views' 2-level form, a fractional vertical shift) and a horizontal
+    list on a forced scalar variant (double-buffered bands); fused sweep and
+    cost volume, bit for bit."""
+    if geom == "c4_knn5":
+        aw, ah, W, H, dmax, bl, zs = 8, 4, 136, 45, 127, 1.0359, (0, 5, 13, 31)
+        cam = _array(aw, ah, 0, dmax, knn=5, bl=bl)
+    else:
+        aw, ah, W, H, dmax, bl, zs = 5, 1, 150, 27, 63, 1.0, (0, 2)
+        cam = _array(aw, ah, 0, dmax, nh=4)
+        eng.set_ncc_variant(8, 4, 192, False)
+    stack, _ = synth.make_stack(W, H, aw, ah, 0, dmax, bl, 0xB0F + W)
+    lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
+    box = eng.box_stats(l8, 5)
+    l8h = l8.cpu().numpy()
+    for z in zs:
+        want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, bl, 5, z)
+        od, oc = orc.wta(want, cam.levels)
+        for form in ("1", "0"):
+            monkeypatch.setenv("MVS_NCC_PLANE32", form)
+            fd, fc = eng.ncc_wta(l8, box, cam, z, 5)
+            assert eng.ncc_last_variant()["DPW"] < 16  # a scalar kernel
+            same(fd, od, f"fused disp z{z} plane32={form}")
+            same(fc, oc, f"fused conf z{z} plane32={form}")
+            vol = eng.ncc_volume(l8, box, cam, z, 5)
+            same(vol, want, f"volume z{z} plane32={form}")
+        monkeypatch.delenv("MVS_NCC_PLANE32")

@@ -56,7 +56,8 @@ namespace {
 // step's tymax), 16 NDB levels per chunk.
 struct alignas(128) NccMRec {
   int txmax, tymax;  // band origin, as NccRec
-  int bhp, shp;      // pk / stats pair rows to stage | (column span) << 16, as NccRec
+  int bhp, shp;      // pk pair rows to stage; stats pair rows (bits 0..7) | the stats bank shift (signed,
+                     // bits 8..15) | column span << 16 | the odd pk rows' bank shift (signed) << 24
   int colo[16];      // 32 x int16: per level j of the chunk, txmax - tx(j) (band column of reference column x0)
                      // | o_j << 8 (VERT: band row of the level's footprint)
   int pad0[2];
@@ -143,10 +144,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   const int lane_x = x0 + lane;
   auto stage_h = [&](const StepInfo& e, int b) {
     if (DBG == 2) return;
-    const int span = e.shp >> 16, nblk = (span + 127) >> 6;
+    const int span = (e.shp >> 16) & 0xff, nblk = (span + 127) >> 6;
     const unsigned long long vo = (unsigned long long)e.hi << 32 | e.lo;
-    u32x4* npk = nbase + b * nbuf;
-    u32x4* nst = npk + a.pk_pairs * BWP;
+    // odd pk pair rows land sh columns along, and (K = 7) stats pair rows 2, 3
+    // st columns along (the step's bank shifts, see step())
+    u32x4* npk = nbase + b * nbuf + ((wave & 1) ? (e.shp >> 24) : 0);
+    u32x4* nst = nbase + b * nbuf + a.pk_pairs * BWP + ((K == 7 && wave >= 2) ? ((e.shp << 16) >> 24) : 0);
     // the wave's roles (pk row w < bhp, stats row w < shp) decided once per step, not per piece
     if (wave < shp) {
       const __amdgpu_buffer_rsrc_t rp =
@@ -172,7 +175,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   auto stage = [&](int t, int n, int b) {
     if (DBG == 2) return;
     const NccMRec& e = rec[t];
-    const int span = e.shp >> 16, nblk = (span + 127) >> 6;
+    const int span = (e.shp >> 16) & 0xff, nblk = (span + 127) >> 6;  // (VERT: no odd-row shift)
     const long vo = (long)a.view[ref][n] * Pv;
     u32x4* npk = nbase + b * nbuf;
     u32x4* nst = npk + a.pk_pairs * BWP;
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         if (wave < shp) glds_b128(stats + vo + st_row + 2 * xx, nst + wave * BWP + c0);
       }
     } else {
-      const int ebh = e.bhp, esh = e.shp & 0xffff;
+      const int ebh = e.bhp, esh = e.shp & 0xff;
       const int pm0 = (y0 - R - e.tymax) >> 1, sm0 = (y0 - e.tymax) >> 1;  // floor: arithmetic shifts
       for (int cb = 0; cb < nblk; cb++) {
         const int c0 = min(cb * 64, span);
@@ -385,9 +388,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // never left of a valid cell's neighbour column - 1 >= 2: nothing to fix)
     if (K == 5 && (VERT || x0 < a.txmax_all)) {  // (tiles right of every shift: never)
       const int jf = (VERT ? rec[t].txmax : cur.tx) - x0 - 1;  // band column of image column -1 (scalar)
-      if (jf >= 0 && jf + 1 < 64 + ((VERT ? rec[t].shp : cur.shp) >> 16)) {  // inside the band's 64 + span columns
+      const int esh = VERT ? rec[t].shp : cur.shp;
+      if (jf >= 0 && jf + 1 < 64 + ((esh >> 16) & 0xff)) {  // inside the band's 64 + span columns
         if (tid < a.pk_pairs) {
-          u32x4* e = nbuf_t + tid * BWP + jf;
+          u32x4* e = nbuf_t + tid * BWP + jf + ((tid & 1) ? (esh >> 24) : 0);
           const u32x4 v = e[1];
           *e = u32x4{v.x << 8, (v.y << 8) | (v.x >> 24), v.z << 8, (v.w << 8) | (v.z >> 24)};
         }
@@ -400,7 +404,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     } else if constexpr (!VERT) {
       if (t + 2 < T) {
         stage_h(nx2, bt == 0 ? 2 : bt - 1);  // (t + 2) % 3
-        const int nb2 = ((nx2.shp >> 16) + 127) >> 6;
+        const int nb2 = (((nx2.shp >> 16) & 0xff) + 127) >> 6;
         pieces = (wave < bhp ? nb2 : 0) + (wave < shp ? nb2 : 0);
       }
     } else {
@@ -430,10 +434,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         iS1[db] = 4 * ((s1 >> 1) * BWP + col + g) + (s1 & 1);
       }
     }
+    // The lanes reading odd pk pair rows (g odd) find them sh columns along,
+    // the step's bank shift: with the pitch BW + 1, lanes of one ds_read_b128
+    // group read two rows 1 + sh bank quads apart, and the host picks sh per
+    // step so that the column shift per level (|dx| = 1, 3 want sh = -1; 2
+    // wants 0) puts their 16-byte entries on distinct quads.  K = 7: the odd-g
+    // lanes' stats pairs (2, 3) likewise, st columns along
+    const int sg = (!VERT && (g & 1)) ? (cur.shp >> 24) : 0;
+    const int tg = (K == 7 && (g & 1)) ? ((cur.shp << 16) >> 24) : 0;
     auto bread = [&](int xb, int yb, int db, int mf) -> i32x4 {
-      if constexpr (!VERT) {  // K = 5: pair 2 yb + g of the band; K = 7: pair g + 4 mf
+      if constexpr (!VERT) {  // K = 5: pair 2 yb + g of the band; K = 7: pair g + 4 mf (parity g & 1 alike)
         const int pr = K == 5 ? 2 * yb + g : g + 4 * mf;
-        return __builtin_bit_cast(i32x4, npk[pr * BWP + 8 * wave + BXW * xb + cl[db]]);
+        return __builtin_bit_cast(i32x4, npk[pr * BWP + 8 * wave + BXW * xb + cl[db] + sg]);
       } else {
         const uint2* b2 = (const uint2*)npk;
         const int off = 2 * (2 * yb * BWP + 4 * xb);
@@ -444,7 +456,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // {a, a, b, b} of pixel rows 0, 1 (s0) and rows 2, 3 (s1) of the block
     auto sread = [&](int xb, int yb, int db, f32x4& s0, f32x4& s1) {
       if constexpr (!VERT) {
-        const int colS = 8 * wave + pcol(xb, g) + cl[db];  // stats band column of this lane's pixel column
+        const int colS = 8 * wave + pcol(xb, g) + cl[db] + tg;  // stats band column of this lane's pixel column
         const int sp = prow(yb, g) >> 1;                    // stats band pair of its first row
         s0 = __builtin_bit_cast(f32x4, nst[sp * BWP + colS]);
         s1 = __builtin_bit_cast(f32x4, nst[(sp + 1) * BWP + colS]);
@@ -649,6 +661,76 @@ int launch_vert(mvs_ctx* ctx, const uint2* stats, const uint2* pk, const NccMRec
 
 }  // namespace
 
+// LDS cycles of the B-operand / stats ds_read_b128 of one step (MI355X_MICROARCH.md,
+// LDS table): 4 groups of 16 lanes, one cycle per group plus one per further
+// distinct 16-byte entry on a busy bank quad (entry index mod 16; identical
+// entries broadcast); summed over the chunk's level blocks and the 16
+// residues c of the block column.  Lane l = 16 g + n reads entry
+// row(g) (BW + 1) + sh (g & 1) + col(g) + c + colo[n], BW + 1 = 1 mod 16 for
+// every horizontal pitch (129, 193): B operands row(g) = g, col(g) = 0;
+// K = 7 stats row(g) = 2 (g & 1), col(g) = g >> 1.  (K = 5 stats: every lane
+// of a read on one row, column g -- no shift changes them.)
+static int bank_cycles(const int16_t* colo, int dc, int sh, bool k7_stats) {
+  static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  // (a residue c adds to every entry alike: it rotates the quads and leaves
+  // the count unchanged, so c = 0 stands for all 16)
+  int cyc = 0;
+  for (int b0 = 0; b0 < dc; b0 += 16)
+      for (const auto& gr : grp) {
+        int ent[16], most = 1;
+        for (int i = 0; i < 16; i++) {
+          const int l = gr[i], g = l >> 4;
+          const int row = k7_stats ? 2 * (g & 1) : g, col = k7_stats ? g >> 1 : 0;
+          ent[i] = row * 129 + sh * (g & 1) + col + (colo[b0 + (l & 15)] & 0xff) + 64;
+        }
+        for (int q = 0; q < 16; q++) {  // distinct entries on bank quad q
+          int n = 0;
+          for (int i = 0; i < 16; i++) {
+            if ((ent[i] & 15) != q) continue;
+            bool dup = false;
+            for (int k = 0; k < i; k++) dup |= ent[k] == ent[i];
+            n += !dup;
+          }
+          most = std::max(most, n);
+        }
+        cyc += most;
+      }
+  return cyc;
+}
+// the shift of fewest cycles among those the band's slack allows (a shifted
+// row must stay inside its BW + 1 slot: |sh| <= BW + 1 - band_w; ties: the
+// smaller |sh|, then the negative one)
+static int bank_shift_eval(const int16_t* colo, int dc, bool k7_stats, int slack) {
+  int best = 0, best_cyc = bank_cycles(colo, dc, 0, k7_stats);
+  for (int sh : {-1, 1, -2, 2}) {
+    if (std::abs(sh) > slack) continue;
+    const int c = bank_cycles(colo, dc, sh, k7_stats);
+    if (c < best_cyc) {
+      best_cyc = c;
+      best = sh;
+    }
+  }
+  return best;
+}
+// memoised: the plan is rebuilt per call, and a level block's offsets repeat
+// from call to call (a pure function of them, shared by every context)
+static int bank_shift(const int16_t* colo, int dc, bool k7_stats, int slack) {
+  static std::mutex mu;
+  static std::map<std::vector<int16_t>, int> memo;
+  std::vector<int16_t> key(colo, colo + dc);
+  key.push_back((int16_t)(k7_stats ? 1 : 0));
+  key.push_back((int16_t)std::min(slack, 2));  // (shifts beyond 2 are never tried)
+  std::lock_guard<std::mutex> lock(mu);
+  const auto it = memo.find(key);
+  if (it != memo.end()) return it->second;
+  const int v = bank_shift_eval(colo, dc, k7_stats, slack);
+  memo.emplace(std::move(key), v);
+  return v;
+}
+
 // the matrix-core form's plan: one NccMRec per (chunk of 16 ndb levels, neighbour)
 NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, const float* fdy, float bl, int ndb,
                         int K) {
@@ -688,6 +770,15 @@ NccPlanM make_plan_mfma(const float* levels, int D, int nn, const float* fdx, co
         const int dl = c * DC + j;
         // a dummy level past the end: the band origin (in-band)
         co[j] = (int16_t)(dl < D ? (txmax - tx_of(dl, n)) | ((par + tymax - ty_of(dl, n)) << 8) : par << 8);
+      }
+      // horizontal lists: the odd pk rows' shift (bits 24..31 of word 3) and,
+      // K = 7, the stats rows' (bits 8..15) that leave step()'s reads the
+      // fewest LDS cycles.  Slack: the band pitch BW + 1 (129 | 193, the
+      // horizontal templates) less this step's 64 + span columns
+      if (!p.vert) {
+        const int bw = 64 + txmax - txmin, slack = (bw <= 128 ? 129 : 193) - bw;
+        e[3] |= (bank_shift(co, DC, false, slack) & 0xff) << 24;
+        if (K == 7) e[3] |= (bank_shift(co, DC, true, slack) & 0xff) << 8;
       }
       spx = std::max(spx, txmax - txmin);
       p.pk_pairs = std::max(p.pk_pairs, bhp);

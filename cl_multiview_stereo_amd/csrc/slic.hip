@@ -914,6 +914,15 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
       (void*)(labels ? labels + (long)z * P : nullptr), 0, labels ? (int)(P * 4) : 0, 0x00020000);
   uint32_t lbl[4];
   int win[4];  // the pixel's candidate (-1: none, or outside the image)
+  // the lane's column is the same for its 4 pixels: (x - cx)^2 of each
+  // candidate once (the same product slic_dist2 forms, so the same bits)
+  f32x2 bcx[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const float colf = (float)(TX * 16 + lx);
+    const f32x2 dx = f32x2{colf, colf} - ccxp[h];
+    bcx[h] = dx * dx;
+  }
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const int col = TX * 16 + lx, row = TY * 16 + ly0 + 4 * m;
@@ -928,8 +937,7 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
       ac = ac + da * da;
       const f32x2 db = f32x2{c[m].z, c[m].z} - cbp[h];
       ac = ac + db * db;
-      const f32x2 dx = f32x2{(float)col, (float)col} - ccxp[h];
-      f32x2 bc = dx * dx;
+      f32x2 bc = bcx[h];
       const f32x2 dy = f32x2{(float)row, (float)row} - ccyp[h];
       bc = bc + dy * dy;
       const f32x2 d = (ac * f32x2{col_n, col_n}) + f32x2{weight, weight} * (bc * f32x2{xy_n, xy_n});
@@ -942,17 +950,20 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
     // (d2 * 0.99999905 <= least: k_assign's own near-tie test), or the least
     // is not below the 9e11 the first take is sure of.  Such a lane re-runs
     // k_assign's loop.  NaN (outside-map) candidates drop out of the min.
-    const float lo = fminf(fminf(d2[0], d2[1]), fminf(d2[2], d2[3]));
+    // v_min3 / v_min (IEEE minNum: a quiet-NaN operand drops out, as in fminf;
+    // as asm, without the canonicalising v_max fminf brings along)
+    float lo, lo01;
+    asm("v_min_f32 %0, %1, %2" : "=v"(lo01) : "v"(d2[0]), "v"(d2[1]));
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(lo) : "v"(lo01), "v"(d2[2]), "v"(d2[3]));
     int w = d2[3] == lo ? 3 : -1;
     w = d2[2] == lo ? 2 : w;
     w = d2[1] == lo ? 1 : w;
     w = d2[0] == lo ? 0 : w;
-    // (as float maxima, not short-circuit logic, which compiled to a branch
-    // per candidate: lo - x >= 0 iff x <= lo for finite x)
-    float am = lo < 9.0e11f ? -1.0f : 1.0f;
+    // (bitwise, not short-circuit logic, which compiled to a branch per
+    // candidate: the compares combine as lane masks on the scalar unit)
+    bool amb = !(lo < 9.0e11f);
 #pragma unroll
-    for (int i = 0; i < 4; i++) am = fmaxf(am, d2[i] > lo ? lo - d2[i] * 0.99999905f : -1.0f);
-    const bool amb = am >= 0.0f;
+    for (int i = 0; i < 4; i++) amb |= (d2[i] > lo) & (d2[i] * 0.99999905f <= lo);
     float min_id = w == 0 ? cid[0] : w == 1 ? cid[1] : w == 2 ? cid[2] : w == 3 ? cid[3] : -1.0f;
     if (amb) {  // k_assign's loop, square roots and all
       float best2 = 0.0f;

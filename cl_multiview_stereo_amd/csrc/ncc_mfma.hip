@@ -326,16 +326,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
           f32x2 cst[NDB];
 #pragma unroll
           for (int db = 0; db < NDB; db++) {
-            const f32x2 e = f32x2{E[kb][db][r], E[kb][db][r + 1]} * f32x2{sq[r], sq[r + 1]};
+            f32x2 e;
+            e.x = __fmul_rn(E[kb][db][r], sq[r]);
+            e.y = __fmul_rn(E[kb][db][r + 1], sq[r + 1]);
             // NDB = 2: 1 - m without the clamp max(-1, m) -- a cost above 2 or
             // NaN (no valid neighbour window at the level) stands for the
             // clamped 2, restored at the merge; the pair fold below treats NaN
             // as absent.  (NDB = 1 keeps the clamp: its med3 fold would not.)
-            if constexpr (NDB == 2)
-              cst[db] = f32x2{1.0f, 1.0f} - e;
-            else
-              cst[db] = f32x2{1.0f, 1.0f} - f32x2{vmax_m1(e.x), vmax_m1(e.y)};
-            if (TAIL) cst[db] += f32x2{kill[db], kill[db]};  // costs are >= 0: x + 0 = x, x + inf = inf
+            if constexpr (NDB == 2) {
+              cst[db].x = __fsub_rn(1.0f, e.x);
+              cst[db].y = __fsub_rn(1.0f, e.y);
+            } else {
+              cst[db].x = __fsub_rn(1.0f, vmax_m1(e.x));
+              cst[db].y = __fsub_rn(1.0f, vmax_m1(e.y));
+            }
+            if (TAIL) {  // costs are >= 0: x + 0 = x, x + inf = inf
+              cst[db].x = __fadd_rn(cst[db].x, kill[db]);
+              cst[db].y = __fadd_rn(cst[db].y, kill[db]);
+            }
           }
 #pragma unroll
           for (int h = 0; h < 2; h++) {
@@ -473,9 +481,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
       for (int p = 0; p < 2; p++) {
         const f32x4 sv = p ? s1 : s0;
-        const f32x2 f = f32x2{__int_as_float(acc[2 * p]), __int_as_float(acc[2 * p + 1])} - f32x2{kMagicF, kMagicF};
-        const f32x2 xv = __builtin_elementwise_fma(f32x2{nsr[2 * p], nsr[2 * p + 1]}, f32x2{sv.z, sv.w},
-                                                   f * f32x2{sv.x, sv.y});
+        f32x2 xv;
+        xv.x = __fmaf_rn(nsr[2 * p], sv.z, __fmul_rn(__fsub_rn(__int_as_float(acc[2 * p]), kMagicF), sv.x));
+        xv.y = __fmaf_rn(nsr[2 * p + 1], sv.w, __fmul_rn(__fsub_rn(__int_as_float(acc[2 * p + 1]), kMagicF), sv.y));
         const int kb = xb * NYB + yb;
         if (FIRST) {
           E[kb][db][2 * p] = xv.x;

@@ -33,7 +33,9 @@ namespace {
 // exactly the pk plane's row-pair entry, so a lane's B operand for row pair g
 // is ONE ds_read_b128 from the band the LDS-DMA stages anyway.  The MFMA's
 // accumulator starts at the bits of 1.5 * 2^23: read as a float the result is
-// 1.5 * 2^23 + Srp' exactly (|Srp'| < 2^22), one v_pk_add_f32 per 2 cells.
+// 1.5 * 2^23 + Srp' exactly (|Srp'| < 2^22), one v_sub_f32 per cell (scalar
+// f32 throughout the finish and fold: v_pk_*_f32 measured slower, C2 -1.3 %,
+// C5 -3.2 %, profiles/r06/ab_scalar_f32_finish.txt).
 // Per lane the output is C[4 (l >> 4) + r][l & 15]: pixel column xx = l >> 4,
 // rows yy = r = 0..3, level l & 15 -- a fixed pixel column and level per lane,
 // so the neighbour stats (a, b of rows y0b..y0b+3 at column x - tx) are two

@@ -916,33 +916,30 @@ __global__ __launch_bounds__(256) void k_assign_tiles4(const float4* __restrict_
   int win[4];  // the pixel's candidate (-1: none, or outside the image)
   // the lane's column is the same for its 4 pixels: (x - cx)^2 of each
   // candidate once (the same product slic_dist2 forms, so the same bits)
-  f32x2 bcx[2];
+  float bcx[4];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const float colf = (float)(TX * 16 + lx);
-    const f32x2 dx = f32x2{colf, colf} - ccxp[h];
-    bcx[h] = dx * dx;
+  for (int i = 0; i < 4; i++) {
+    const float dx = __fsub_rn((float)(TX * 16 + lx), ccxp[i >> 1][i & 1]);
+    bcx[i] = __fmul_rn(dx, dx);
   }
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const int col = TX * 16 + lx, row = TY * 16 + ly0 + 4 * m;
-    // slic_dist2 for two candidates at once (packed FP32, the same operations
-    // in the same order)
+    // slic_dist2 per candidate, the same operations in the same order, in
+    // scalar f32 (v_pk_*_f32 measured slower in the NCC kernels)
     float d2[4];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const f32x2 dl = f32x2{c[m].x, c[m].x} - cLp[h];
-      f32x2 ac = dl * dl;
-      const f32x2 da = f32x2{c[m].y, c[m].y} - cap[h];
-      ac = ac + da * da;
-      const f32x2 db = f32x2{c[m].z, c[m].z} - cbp[h];
-      ac = ac + db * db;
-      f32x2 bc = bcx[h];
-      const f32x2 dy = f32x2{(float)row, (float)row} - ccyp[h];
-      bc = bc + dy * dy;
-      const f32x2 d = (ac * f32x2{col_n, col_n}) + f32x2{weight, weight} * (bc * f32x2{xy_n, xy_n});
-      d2[2 * h] = d.x;
-      d2[2 * h + 1] = d.y;
+    for (int i = 0; i < 4; i++) {
+      const int h = i >> 1, k = i & 1;
+      const float dl = __fsub_rn(c[m].x, cLp[h][k]);
+      float ac = __fmul_rn(dl, dl);
+      const float da = __fsub_rn(c[m].y, cap[h][k]);
+      ac = __fadd_rn(ac, __fmul_rn(da, da));
+      const float db = __fsub_rn(c[m].z, cbp[h][k]);
+      ac = __fadd_rn(ac, __fmul_rn(db, db));
+      const float dy = __fsub_rn((float)row, ccyp[h][k]);
+      const float bc = __fadd_rn(bcx[i], __fmul_rn(dy, dy));
+      d2[i] = __fadd_rn(__fmul_rn(ac, col_n), __fmul_rn(weight, __fmul_rn(bc, xy_n)));
     }
     // k_assign's loop keeps the first candidate of least sqrtf(d2) (strict <),
     // sqrtf being monotone: the first of least d2, unless a later-looking d2

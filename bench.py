@@ -512,7 +512,7 @@ def bench(args, world, rank, local):
         nbr = max(1, int(pipe.cam.subset_num[0]))
         per_view = _valu_insts_fused_per_view(args.config, W, H, D)
         res["roofline_sweep"] = {
-            "kernel": "fused sweep + WTA (k_ncc_mfma for K = 5 horizontal lists, else k_ncc_volume<..., FUSE=true>): the headline step's dominant kernel",
+            "kernel": "fused sweep + WTA (k_ncc_mfma: K = 5 lists, K = 7 horizontal lists; k_ncc_volume<..., FUSE=true> where its bands miss the LDS): the headline step's dominant kernel",
             "bound": "valu", "avg_call_ms": round(t_f * 1e3, 4), "views_per_call": vpc,
             "avg_ms_per_view": round(t_f * 1e3 / vpc, 4),
             "view_cells_per_s": round(cells * nbr * vpc / t_f / 1e9, 3), "unit_view_cells": "G view-cells/s",

@@ -798,9 +798,10 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   // single-buffered, 16-level double- / single-buffered chunks whose bands
   // leave two workgroups per CU (80 KB).  MVS_NCC_MFMA=0 (read per call) or a
   // forced variant (mvs_set_ncc_variant) keeps the scalar kernels.  VERT
-  // lists take the matrix-core form only with MVS_NCC_MFMA_V=1 (that choice)
-  // or 22 | 21 | 12 | 11 (chunk blocks, buffers: that form): C4's tall bands
-  // keep it DMA-bound and slower than the scalar kernels
+  // lists take the matrix-core form by default (MVS_NCC_MFMA_V unset or 1:
+  // the launcher's choice under two workgroups per CU; 22 | 21 | 12 | 11:
+  // that form; 0: the scalar kernels).  Since its finish went scalar f32 it
+  // runs C4's 5-NN lists ~1 % faster than the scalar kernels
   // K = 7 (C5): horizontal lists in 16-level chunks (its 2 x 8-pixel blocks'
   // operands take 32 VGPRs); MVS_NCC_MFMA7=0 keeps the scalar kernels (A/B)
   const char* mfe = getenv("MVS_NCC_MFMA");
@@ -810,7 +811,7 @@ int launch_ncc_refs(mvs_ctx* ctx, int V, int W, int H, const int32_t* box, const
   const bool mf_on = !vol && (K == 5 || (K == 7 && !(mf7 && atoi(mf7) == 0))) && !(mfe && atoi(mfe) == 0) &&
                      !ctx->ncc_nw && !ctx->ncc_dpw && !ctx->ncc_general && !ctx->ncc_bw &&
                      (long)W * (H + (H & 1)) * 8 < 0x7fffffffL;
-  const int mfv_form = mfv ? atoi(mfv) : 0;  // 0: off, 1: automatic, else the form
+  const int mfv_form = mfv ? atoi(mfv) : 1;  // 0: off, 1: automatic (default), else the form
   std::vector<char> mf(n, 0);
   std::vector<NccPlanM> mplan(n);
   std::vector<int> mnb(n, 2);

@@ -44,7 +44,7 @@ def main():
     knn = params.nearest_neighbours(aw, ah, 5)
     cases = {"h1": {z: [z + 1]}, "h2": {z: [z - 1, z + 1]}, "v1": {z: [z + aw]}, "v2": {z: [z - aw, z + aw]},
              "d1": {z: [z + aw + 1]}, "knn5": {z: knn[z]}, "corner0": {0: knn[0]}}
-    forms = [("scalar", {}), ("22", {"MVS_NCC_MFMA_V": "22"}), ("21", {"MVS_NCC_MFMA_V": "21"}),
+    forms = [("scalar", {"MVS_NCC_MFMA_V": "0"}), ("22", {"MVS_NCC_MFMA_V": "22"}), ("21", {"MVS_NCC_MFMA_V": "21"}),
              ("12", {"MVS_NCC_MFMA_V": "12"}), ("11", {"MVS_NCC_MFMA_V": "11"}),
              ("12_nocompute", {"MVS_NCC_MFMA_V": "12", "MVS_NCC_MFMA_DBG": "1"}),
              ("12_nodma", {"MVS_NCC_MFMA_V": "12", "MVS_NCC_MFMA_DBG": "2"})]

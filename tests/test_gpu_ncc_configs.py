@@ -159,8 +159,9 @@ def test_mfma_vertical_forms(eng, form, bl, dmax, H, monkeypatch):
     """The matrix-core fused sweep for lists with vertical / diagonal
     neighbours (k_ncc_mfma<..., VERT>: C4's 8x4 array, 5 nearest neighbours),
     every view of the array, each (16-level blocks per chunk, band buffers)
-    form forced through MVS_NCC_MFMA_V ("auto", MVS_NCC_MFMA_V=1: the
-    launcher's choice under two workgroups per CU; unset: the scalar kernels).  D = 128 (whole chunks) and D = 100 (dummy levels
+    form forced through MVS_NCC_MFMA_V ("auto", MVS_NCC_MFMA_V=1 or unset:
+    the launcher's choice under two workgroups per CU, the default; 0: the
+    scalar kernels).  D = 128 (whole chunks) and D = 100 (dummy levels
     in the last chunk); bl = 1.0359: fractional vertical shifts, so a chunk's
     levels start on odd and even band rows; H = 69: an odd height (the dummy
     row of the pair planes) and a partial last tile row."""
@@ -470,6 +471,7 @@ def test_scalar_band_dma_forms(eng, monkeypatch, geom):
     lab, l8 = eng.cvt(torch.from_numpy(stack).cuda())
     box = eng.box_stats(l8, 5)
     l8h = l8.cpu().numpy()
+    monkeypatch.setenv("MVS_NCC_MFMA_V", "0")  # the scalar kernels for the vertical lists too
     for z in zs:
         want = orc.ncc_volume(l8h, cam.levels, cam.view_subset, cam.subset_num, aw, bl, 5, z)
         od, oc = orc.wta(want, cam.levels)

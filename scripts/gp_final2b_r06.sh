@@ -1,0 +1,20 @@
+# round-6 final records, second session (part B: suite, lines, traces): PMC passes and kernel traces of the C2
+# and C5 bench steps (the NCC sources changed: profiles/pmc_*.json carry their
+# hash), the headline kernel's SQ counters, the GPU suite, smoke, the driver's
+# bench command and every other configuration's line, a kernel trace of the
+# driver's command with the trace-vs-line check, and the C4 replay bound.
+# Summaries under gpurun_out/r06z; rocprof databases removed (64 MiB cap).
+set -u
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r06z; mkdir -p $O
+bash scripts/gpu_pass.sh r06z tests smoke bench bench:c1 bench:c3 bench:c4 bench:c5 bench:ref || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace_drv -o run -- python3 bench.py --gpus 1 --steps 20 \
+  --warmup 5 > $O/trace_driver_bench.json 2> $O/trace_drv.err || { tail -5 $O/trace_drv.err; exit 1; }
+python3 scripts/kstats.py $O/trace_drv > $O/c2_driver_kernel_trace.txt 2>&1
+python3 scripts/headline_kernel_check.py $O/trace_drv $O/trace_driver_bench.json 20 5 > $O/headline_check.json 2>&1
+cat $O/headline_check.json
+rm -rf $O/trace_drv
+timeout -k 10 600 python3 scripts/c4_shard_sim.py --world 8 --steps 3 > $O/c4_shard_sim.json 2> $O/c4_shard_sim.err || { tail -5 $O/c4_shard_sim.err; exit 1; }
+cat $O/c4_shard_sim.json | head -c 600
+du -sh gpurun_out

@@ -737,6 +737,7 @@ static int bank_shift(const int16_t* colo, int dc, bool k7_stats, int slack) {
   const auto it = memo.find(key);
   if (it != memo.end()) return it->second;
   const int v = bank_shift_eval(colo, dc, k7_stats, slack);
+  if (memo.size() >= (1u << 16)) memo.clear();  // bounded: ~64 K level blocks (a few MB)
   memo.emplace(std::move(key), v);
   return v;
 }

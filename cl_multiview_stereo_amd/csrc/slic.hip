@@ -297,34 +297,71 @@ __global__ __launch_bounds__(256) void k_assign(const float4* __restrict__ lab, 
     // order).  sqrt is monotone, so a candidate with d2 >= the best d2 never
     // wins, and one below it by more than 2^-20 relative always does; only a
     // near tie needs the two correctly rounded square roots compared.
-    float best2 = 0.0f, min_id = -1.0f;
-    bool have = false;
+    float min_id = -1.0f;
     constexpr int NC = S3 ? 3 : 2;
+    // the reference's loop, square roots and all
+    auto exact = [&]() {
+      float best2 = 0.0f, mid = -1.0f;
+      bool have = false;
 #pragma unroll
-    for (int ii = 0; ii < NC; ii++)
+      for (int ii = 0; ii < NC; ii++)
 #pragma unroll
-      for (int jj = 0; jj < NC; jj++) {
+        for (int jj = 0; jj < NC; jj++) {
+          int ox, oy;
+          slic_cand<S3>(ii, jj, dX, dY, ox, oy);
+          const int cx = cxg + ox, cy = cyg + oy;
+          const bool ok = cx >= 0 && cy >= 0 && cx < mw && cy < mh;
+          const int e = ok ? (cy - cy0) * ncx + (cx - cx0) : 0;
+          const float d2 = slic_dist2(px, row, col, cxyla[e], cbb[e], weight, xy_n, col_n);
+          bool take;
+          if (!have) {
+            take = d2 < 9.0e11f || sqrtf(d2) < 999999.9999f;  // the reference's initial min_dist
+          } else if (d2 >= best2) {
+            take = false;
+          } else if (d2 < best2 * 0.99999905f) {
+            take = true;
+          } else {
+            take = sqrtf(d2) < sqrtf(best2);
+          }
+          take = take && ok;
+          best2 = take ? d2 : best2;
+          mid = take ? (float)(cy * mw + cx) : mid;
+          have = have || take;
+        }
+      return mid;
+    };
+    if constexpr (S3) {
+      min_id = exact();
+    } else {
+      // (k_assign_tiles4's test) the loop keeps the first candidate of least
+      // d2 unless another d2 lies within the sqrt rounding above the least
+      // (d2 * 0.99999905 <= least) or the least is not below 9e11: such a
+      // pixel runs the loop itself.  A candidate outside the map takes a NaN
+      // d2: never the least, never a near tie.
+      float d2[4], cid[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
         int ox, oy;
-        slic_cand<S3>(ii, jj, dX, dY, ox, oy);
+        slic_cand<false>(i >> 1, i & 1, dX, dY, ox, oy);
         const int cx = cxg + ox, cy = cyg + oy;
         const bool ok = cx >= 0 && cy >= 0 && cx < mw && cy < mh;
         const int e = ok ? (cy - cy0) * ncx + (cx - cx0) : 0;
-        const float d2 = slic_dist2(px, row, col, cxyla[e], cbb[e], weight, xy_n, col_n);
-        bool take;
-        if (!have) {
-          take = d2 < 9.0e11f || sqrtf(d2) < 999999.9999f;  // the reference's initial min_dist
-        } else if (d2 >= best2) {
-          take = false;
-        } else if (d2 < best2 * 0.99999905f) {
-          take = true;
-        } else {
-          take = sqrtf(d2) < sqrtf(best2);
-        }
-        take = take && ok;
-        best2 = take ? d2 : best2;
-        min_id = take ? (float)(cy * mw + cx) : min_id;
-        have = have || take;
+        const float v = slic_dist2(px, row, col, cxyla[e], cbb[e], weight, xy_n, col_n);
+        d2[i] = ok ? v : __builtin_nanf("");
+        cid[i] = (float)(cy * mw + cx);
       }
+      float lo, lo01;
+      asm("v_min_f32 %0, %1, %2" : "=v"(lo01) : "v"(d2[0]), "v"(d2[1]));
+      asm("v_min3_f32 %0, %1, %2, %3" : "=v"(lo) : "v"(lo01), "v"(d2[2]), "v"(d2[3]));
+      bool amb = !(lo < 9.0e11f);
+#pragma unroll
+      for (int i = 0; i < 4; i++) amb |= (d2[i] > lo) & (d2[i] * 0.99999905f <= lo);
+      min_id = d2[3] == lo ? cid[3] : -1.0f;
+      min_id = d2[2] == lo ? cid[2] : min_id;
+      min_id = d2[1] == lo ? cid[1] : min_id;
+      min_id = d2[0] == lo ? cid[0] : min_id;
+      if (amb) min_id = exact();
+    }
     if (labels) labels[pid] = (uint32_t)min_id;  // (null: an update follows, reading only the copy)
     if (lb16) lb16[pid] = (uint16_t)min_id;      // the next k_update's 16-bit copy (mw * mh <= 65536)
   }

@@ -1079,6 +1079,10 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
   long M = (long)mw * mh;
   int wps = (D + 63) / 64;
   wps = wps >= 3 ? 4 : wps;  // waves per superpixel: 1, 2 or 4
+  // MVS_SWEEP_WPS=1|2|4 (read per call): another wave count per superpixel (A/B)
+  const char* we = getenv("MVS_SWEEP_WPS");
+  const int wps_env = (we && D > 32 && (atoi(we) == 1 || atoi(we) == 2 || atoi(we) == 4)) ? atoi(we) : 0;
+  if (wps_env) wps = wps_env;
   const bool half = D <= 32;  // two superpixels per wave
   const int spb = half ? 8 : 4 / wps;
   SweepArgs a{V, W, H, mw, mh, D, aw, z0, bl};
@@ -1169,10 +1173,17 @@ int launch_sweep_spixl(mvs_ctx* ctx, int V, int W, int H, int S, const float* la
     if (2.0 * (S - 1) + 2.0 + (double)rng * mdx + 1.0 > (double)kSwU) ring_ok = false;
   }
   if (ring_ok) {
-    const dim3 g((unsigned)(8 * ((nb + 7) / 8)), (unsigned)(z1 - z0));
-    if (wps == 1)
+    // one wave per superpixel, its 64-level passes in turn: the ring form's
+    // cost is per staged row and level, not per wave, and four superpixels per
+    // workgroup share its setup and tail (C5, D = 256: 1.19 ms per launch
+    // against 1.42 with four waves per superpixel; C2 alike at 1 and 2:
+    // profiles/r06/sweep_ring_waves.txt)
+    const int rw = wps_env ? wps_env : 1;
+    const long nbr = (M + 4 / rw - 1) / (4 / rw);
+    const dim3 g((unsigned)(8 * ((nbr + 7) / 8)), (unsigned)(z1 - z0));
+    if (rw == 1)
       hipLaunchKernelGGL(k_sweep_spixl_ring<1>, g, dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a);
-    else if (wps == 2)
+    else if (rw == 2)
       hipLaunchKernelGGL(k_sweep_spixl_ring<2>, g, dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a);
     else
       hipLaunchKernelGGL(k_sweep_spixl_ring<4>, g, dim3(256), 0, s, (const float4*)lab, spixl, rep, levels, vs, sn, a);
